@@ -1,0 +1,117 @@
+/*
+ * qtesla_ntt.h -- C ABI of the MI355X (gfx950) batched negacyclic NTT engine.
+ *
+ * Drop-in boundary for the reference benlwk/ntt-gpu-qTESLA (NTT.cu).  The
+ * reference has no library API: its "launch signature" is a family of
+ * per-stage __global__ kernels launched <<<BATCH, T>>> by its test drivers
+ * over caller-allocated, poly-major device buffers [BATCH][NTTSIZE] of
+ * uint32 coefficients in [0,q).  Each entry point below replaces one whole
+ * kernel sequence of those drivers (file:line cited per function) with one
+ * launch of a hand-written CDNA4 kernel.
+ *
+ * Conventions (all entry points):
+ *   - device pointers, poly-major [batch][n] uint32, coefficients in [0,q);
+ *     the caller owns the memory, the library never allocates on the hot path;
+ *   - `stream` is a hipStream_t (NULL = default stream); calls are
+ *     asynchronous on that stream, reentrant across streams and devices;
+ *   - return 0 on success, a negative NTT_ERR_* code otherwise (never abort);
+ *   - `twiddleFactor` is accepted and ignored, exactly like the reference
+ *     kernels' dead parameter (NTT.cu:1436 etc. read __constant__ tables).
+ *   - inputs >= q are a contract violation (the reference silently returns
+ *     non-congruent values for them).  This library tolerates inputs in
+ *     [0, 2q): the output is then the exact canonical result for the input
+ *     reduced mod q (DESIGN.md "lazy reduction bounds").  Outputs are
+ *     always canonical, in [0, q).
+ */
+#ifndef QTESLA_NTT_H
+#define QTESLA_NTT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- parameter sets ---------------------------------------------------- */
+/* reference set: qTESLA-III-speed (round 1), main.cuh:13-21 + constants.h   */
+#define NTT_PARAM_REF 0   /* n = 1024, q = 8404993,   psi = 2083362          */
+#define NTT_PARAM_P_I 1   /* n = 1024, q = 343576577, psi = 3^((q-1)/2n)    */
+#define NTT_PARAM_P_III 2 /* n = 2048, q = 856145921, psi = 3^((q-1)/2n)    */
+
+/* ---- error codes ------------------------------------------------------- */
+#define NTT_OK 0
+#define NTT_ERR_PARAM (-1)   /* unknown param_set                              */
+#define NTT_ERR_NULL (-2)    /* NULL device pointer with batch > 0             */
+#define NTT_ERR_ALIGN (-3)   /* device pointer not 4-byte aligned              */
+#define NTT_ERR_HIP (-4)     /* HIP runtime / launch error (ntt_last_hip_error)*/
+#define NTT_ERR_SIZE (-5)    /* batch too large (batch*n must fit in 2^40)     */
+#define NTT_ERR_ALIAS (-6)   /* forbidden partial overlap of in/out buffers    */
+
+/* Parameter query: any out pointer may be NULL.
+ * Replaces the compile-time macros P / NTTSIZE (main.cuh:14-16) and the root
+ * constants fg0 / ig0 / Ni (main.cu:26). */
+int ntt_param_info(int param_set, uint32_t *n, uint32_t *q, uint32_t *psi,
+                   uint32_t *omega, uint32_t *omega_inv, uint32_t *n_inv);
+
+/* Host copies of the constants.h-equivalent tables, n entries each (any
+ * pointer may be NULL): bitrev_tbl (constants.h:3), Phi = psi^i (:11),
+ * invPhi = n^-1 psi^-i (:19), tf0 = omega^i (:29), ti0 = omega^-i (:33).
+ * For NTT_PARAM_REF they are bit-identical to constants.h. */
+int ntt_get_tables(int param_set, uint32_t *bitrev_tbl, uint32_t *Phi,
+                   uint32_t *invPhi, uint32_t *tf0, uint32_t *ti0);
+
+/* Forward negacyclic NTT, in place, natural order in -> natural order out:
+ *   X[k] = sum_i x_i psi^{(2k+1) i} mod q.
+ * Replaces bit_reverse_copy_tbl_Phi_gpu + radix2NTT_gpu0 x5 + radix2NTT_gpu1 x5
+ * (NTT.cu:2388-2400; kernels :502-509, :1436-1470) -- 12 launches -> 1. */
+int poly_ntt(uint32_t *d_poly, const uint32_t *twiddleFactor, size_t batch,
+             int param_set, void *stream);
+
+/* Inverse negacyclic NTT, in place, natural -> natural (includes n^-1 and
+ * psi^-i, i.e. invPhi):  x_i = n^-1 psi^-i sum_k X[k] omega^-ik.
+ * Replaces GS_radix2INTT_gpu0 x5 + GS_radix2INTT_gpu2 x5 +
+ * bit_reverse_copy_tbl_invPhi_gpu (NTT.cu:2415-2425; kernels :1224-1240,
+ * :1033-1056, :494-500) -- 11 launches -> 1. */
+int poly_invntt(uint32_t *d_poly, const uint32_t *twiddleFactor, size_t batch,
+                int param_set, void *stream);
+
+/* Out-of-place variants (d_out may equal d_in; partial overlap rejected).
+ * Unlike bit_reverse_copy_tbl_Phi_gpu (NTT.cu:506) the input is never
+ * clobbered when d_out != d_in. */
+int poly_ntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch,
+                 int param_set, void *stream);
+int poly_invntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch,
+                    int param_set, void *stream);
+
+/* Fused negacyclic product c = a * b mod (x^n + 1, q), natural order.
+ * Replaces the whole CT-GS pipeline of test_NTT_CT_GS_nega_gpu
+ * (NTT.cu:2388-2425, 34 launches) and CT-CT (NTT.cu:2213-2249) with one
+ * launch; d_c may alias d_a or d_b. */
+int poly_mul(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,
+             size_t batch, int param_set, void *stream);
+
+/* Pointwise product c[i] = a[i] * b[i] mod q over batch*n coefficients.
+ * Replaces pointwise_mult (NTT.cu:1155-1160). */
+int poly_pointwise(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,
+                   size_t batch, int param_set, void *stream);
+
+/* Device-side counter-based generator: coefficient i of poly p gets
+ * splitmix64(seed + (idx+1)*0x9E3779B97F4A7C15) mapped to [0,q) by
+ * multiply-high, idx = (first_poly + p) * n + i.  Lets benchmarks build
+ * multi-GiB inputs on the device; any poly can be regenerated on the host. */
+int ntt_fill_uniform(uint32_t *d_poly, size_t batch, int param_set,
+                     uint64_t seed, uint64_t first_poly, void *stream);
+
+/* Last HIP error code seen by this thread (hipError_t as int), and a
+ * static string for an NTT_ERR_* code. */
+int ntt_last_hip_error(void);
+const char *ntt_strerror(int code);
+
+/* Library / kernel description for reports: writes at most len bytes. */
+int ntt_build_info(char *buf, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QTESLA_NTT_H */

@@ -1,0 +1,868 @@
+// ntt_kernels.hip -- CDNA4 (gfx950) kernels for the batched negacyclic NTT.
+//
+// Replaces the reference's 10-34 per-stage launches per batch (NTT.cu:2388-2425)
+// with one persistent launch per operation.  Geometry (DESIGN.md "kernels"):
+//
+//   * one wave owns one n=2048 polynomial, or two n=1024 polynomials (one per
+//     32-lane half); every lane holds 32 coefficients in VGPRs;
+//   * pass 1: register layout pos = Lp + S*j (S = 64 or 32, j = 0..31); the
+//     five stages on pos bits [LOGN-5, LOGN-1] are in-register radix-2
+//     butterflies with wave-uniform twiddles (scalar loads from __constant__);
+//   * n = 2048 only: the stage on pos bit 5 pairs lanes l and l^32 and runs on
+//     v_permlane32_swap (no LDS);
+//   * one wave-private LDS transpose (conflict-free XOR swizzle, 32 x ds_write_b32
+//     + 8 x ds_read_b128 per lane, no s_barrier) to layout pos = 32*Lp + j;
+//   * pass 2: the five stages on pos bits [0,4] in registers with per-lane
+//     twiddles held in VGPRs for the whole persistent loop;
+//   * forward output is bit-reversed in registers; it is written in natural
+//     order directly: for fixed j the 64 lanes cover one contiguous 256-B chunk.
+//
+// Arithmetic: Harvey lazy butterflies with Shoup (precomputed-quotient
+// Barrett) multiplication, q < 2^30 so 4q < 2^32:
+//   CT: x in [0,4q) -> x' = x mod 2q;  t = y*w mod q in [0,2q);
+//       (x'+t, x'-t+2q) in [0,4q)^2
+//   GS: (x+y reduced to [0,2q), (x-y+2q)*w in [0,2q))
+// Outputs are reduced to canonical [0,q) before they are stored.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+
+#include "../../include/qtesla_ntt.h"
+#include "params.hpp"
+
+namespace qntt {
+
+// ------------------------------------------------------------------------
+// compile-time parameter sets
+// ------------------------------------------------------------------------
+constexpr uint32_t cpow(uint64_t b, uint64_t e, uint64_t q)
+{
+    uint64_t r = 1;
+    b %= q;
+    while (e) {
+        if (e & 1) r = r * b % q;
+        b = b * b % q;
+        e >>= 1;
+    }
+    return (uint32_t)r;
+}
+constexpr uint32_t cshoup(uint32_t w, uint32_t q) { return (uint32_t)(((uint64_t)w << 32) / q); }
+constexpr uint32_t cqinv_neg(uint32_t q)
+{
+    uint32_t inv = q;
+    for (int i = 0; i < 5; i++) inv *= 2u - q * inv;
+    return 0u - inv;
+}
+
+template <uint32_t Q_, int LOGN_, uint32_t PSI_>
+struct PSet {
+    static constexpr uint32_t Q = Q_;
+    static constexpr int LOGN = LOGN_;
+    static constexpr uint32_t N = 1u << LOGN_;
+    static constexpr uint32_t Q2 = 2 * Q_;
+    static constexpr uint32_t QNEG = cqinv_neg(Q_);
+    static constexpr uint32_t NINV = cpow(N, Q_ - 2, Q_);
+    static constexpr uint32_t PSI_INV = cpow(PSI_, Q_ - 2, Q_);
+    // inv twiddle of k = 1 is psi^-brv(1) = psi^-(n/2)
+    static constexpr uint32_t C1 = (uint32_t)((uint64_t)NINV * cpow(PSI_INV, N / 2, Q_) % Q_);
+    static constexpr uint32_t R = (uint32_t)((1ull << 32) % Q_);
+    static constexpr uint32_t NINV_R = (uint32_t)((uint64_t)NINV * R % Q_);
+    static constexpr uint32_t C1_R = (uint32_t)((uint64_t)C1 * R % Q_);
+};
+using PS0 = PSet<8404993u, 10, 2083362u>;
+using PS1 = PSet<343576577u, 10, cpow(3, (343576577u - 1) / 2048, 343576577u)>;
+using PS2 = PSet<856145921u, 11, cpow(3, (856145921u - 1) / 4096, 856145921u)>;
+static_assert(4ull * PS2::Q < (1ull << 32), "lazy bounds need 4q < 2^32");
+
+template <int PS> struct PSel;
+template <> struct PSel<0> { using T = PS0; };
+template <> struct PSel<1> { using T = PS1; };
+template <> struct PSel<2> { using T = PS2; };
+
+// twiddles (w, w'), index k in [0, n): fwd = psi^brv(k), inv = psi^-brv(k)
+__constant__ uint2 c_fwd0[1024];
+__constant__ uint2 c_inv0[1024];
+__constant__ uint2 c_fwd1[1024];
+__constant__ uint2 c_inv1[1024];
+__constant__ uint2 c_fwd2[2048];
+__constant__ uint2 c_inv2[2048];
+
+template <int PS, bool INV>
+__device__ __forceinline__ uint2 twd(uint32_t k)
+{
+    if constexpr (PS == 0) return INV ? c_inv0[k] : c_fwd0[k];
+    else if constexpr (PS == 1) return INV ? c_inv1[k] : c_fwd1[k];
+    else return INV ? c_inv2[k] : c_fwd2[k];
+}
+
+// ------------------------------------------------------------------------
+// modular arithmetic
+// ------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+template <uint32_t Q>
+__device__ __forceinline__ uint32_t shoup_mul(uint32_t a, uint32_t w, uint32_t wp)
+{
+    // a < 2^32, w < q, wp = floor(w 2^32 / q)  ->  result == a*w mod q, in [0, 2q)
+    const uint32_t qe = __umulhi(a, wp);
+    return a * w - qe * Q;
+}
+
+template <uint32_t Q>
+__device__ __forceinline__ void ct_bfly(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp)
+{
+    const uint32_t a = umin(x, x - 2 * Q);       // [0,4q) -> [0,2q)
+    const uint32_t t = shoup_mul<Q>(y, w, wp);   // [0,2q)
+    x = a + t;
+    y = a - t + 2 * Q;
+}
+
+template <uint32_t Q>
+__device__ __forceinline__ void gs_bfly(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp)
+{
+    uint32_t s = x + y;                          // [0,4q)
+    s = umin(s, s - 2 * Q);
+    const uint32_t d = x - y + 2 * Q;            // (0,4q)
+    x = s;
+    y = shoup_mul<Q>(d, w, wp);
+}
+
+// Montgomery product, a,b in [0,2q): returns a*b*2^-32 mod q in [0,2q)
+template <class P>
+__device__ __forceinline__ uint32_t mont_mul(uint32_t a, uint32_t b)
+{
+    const uint32_t lo = a * b;
+    const uint32_t hi = __umulhi(a, b);
+    const uint32_t m = lo * P::QNEG;
+    return hi + __umulhi(m, P::Q) + (lo != 0u ? 1u : 0u);
+}
+
+// ------------------------------------------------------------------------
+// per-lane geometry
+// ------------------------------------------------------------------------
+template <class P>
+struct Lane {
+    static constexpr bool BIG = (P::LOGN == 11);  // one poly per wave
+    static constexpr uint32_t S = BIG ? 64 : 32;  // pass-1 stride
+    uint32_t lane, h, Lp;
+    uint32_t wlo, woff;   // pass-1 LDS write/read (b32) address parts
+    uint32_t rbase, rxm;  // pass-2 LDS read/write (b128) address parts
+    uint32_t brl;         // bit-reversal of Lp over LOGN-5 bits
+
+    __device__ __forceinline__ Lane()
+    {
+        lane = threadIdx.x & 63;
+        h = lane >> 5;
+        Lp = BIG ? lane : (lane & 31);
+        wlo = (lane & 31) ^ (BIG ? (h << 2) : 0u);
+        woff = BIG ? 64 * h : 1024 * h;
+        rxm = (((Lp >> 1) & 1) << 2) | (((Lp >> 2) & 1) << 3) | ((Lp & 1) << 4);
+        rbase = 32 * (Lp ^ ((Lp >> 3) & 1)) + (BIG ? 0u : 1024 * h);
+        brl = __builtin_bitreverse32(Lp) >> (32 - (P::LOGN - 5));
+    }
+};
+
+// XOR swizzle of the wave-private transpose buffer: phys(pos) =
+//   pos ^ (pos6<<2) ^ (pos7<<3) ^ (pos5<<4) ^ (pos8<<5)
+// (bijective; conflict-free for ds_write_b32/ds_read_b32 in the pass-1
+// layouts and ds_read_b128/ds_write_b128 in the pass-2 layout -- checked
+// by tests/test_lds_layout.py against the gfx950 lane-group bank model).
+__host__ __device__ constexpr uint32_t xm_of(uint32_t hi)
+{
+    return (((hi >> 1) & 1) << 2) | (((hi >> 2) & 1) << 3) | ((hi & 1) << 4);
+}
+// pos>>5 of register j in the pass-1 layout (n=2048: after the bit-5 swap)
+template <class P>
+__host__ __device__ constexpr uint32_t hi_of(int j)
+{
+    return P::LOGN == 11 ? (uint32_t)((j & 1) + 4 * (j >> 1)) : (uint32_t)j;
+}
+
+template <class P>
+__device__ __forceinline__ uint32_t p1_addr(const Lane<P> &L, int j)
+{
+    const uint32_t hj = hi_of<P>(j);
+    return (L.wlo ^ xm_of(hj)) + 32 * (hj ^ ((hj >> 3) & 1)) + L.woff;
+}
+
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+// A wave-uniform zero the compiler cannot see through.  Adding it to the
+// index of a uniform twiddle load keeps that load an s_load inside the
+// persistent loop instead of letting LICM hoist all ~126 twiddle words into
+// registers (which cost 2-3 waves/SIMD of occupancy).
+__device__ __forceinline__ uint32_t opaque_zero()
+{
+    uint32_t z = 0;
+    asm volatile("" : "+s"(z));
+    return z;
+}
+
+// pass-1 layout (registers, post-swap for n=2048) -> pass-2 layout
+template <class P>
+__device__ __forceinline__ void lds_p1_to_p2(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
+{
+#pragma unroll
+    for (int j = 0; j < 32; ++j) buf[p1_addr<P>(L, j)] = r[j];
+    compiler_fence();
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(buf + L.rbase + ((4u * c) ^ L.rxm));
+        r[4 * c + 0] = v.x;
+        r[4 * c + 1] = v.y;
+        r[4 * c + 2] = v.z;
+        r[4 * c + 3] = v.w;
+    }
+    compiler_fence();
+}
+
+// pass-2 layout -> pass-1 layout (n=2048: the post-swap arrangement)
+template <class P>
+__device__ __forceinline__ void lds_p2_to_p1(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
+{
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        *reinterpret_cast<uint4 *>(buf + L.rbase + ((4u * c) ^ L.rxm)) =
+            make_uint4(r[4 * c + 0], r[4 * c + 1], r[4 * c + 2], r[4 * c + 3]);
+    compiler_fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) r[j] = buf[p1_addr<P>(L, j)];
+    compiler_fence();
+}
+
+// ------------------------------------------------------------------------
+// transform passes
+// ------------------------------------------------------------------------
+// Table base + an opaque wave-uniform zero: every uniform twiddle read below
+// becomes an s_load_dwordx{2,8,16} with an immediate offset, re-issued per
+// persistent-loop iteration instead of ~126 hoisted words pinning registers.
+template <int PS, bool INV>
+__device__ __forceinline__ const uint2 *tw_base()
+{
+    const uint32_t z = opaque_zero();
+    if constexpr (PS == 0) return (INV ? c_inv0 : c_fwd0) + z;
+    else if constexpr (PS == 1) return (INV ? c_inv1 : c_fwd1) + z;
+    else return (INV ? c_inv2 : c_fwd2) + z;
+}
+
+// forward pass 1: CT stages on pos bits LOGN-1 .. LOGN-5 (j bits 4..0),
+// twiddle index k = 2^s + (j >> (5-s)) -- wave-uniform.
+template <int PS, class P>
+__device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h)
+{
+    const uint2 *tw = tw_base<PS, false>();
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const int hh = 16 >> s;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const uint2 w = tw[(1u << s) + (uint32_t)(j >> (5 - s))];
+                ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+            }
+        }
+    }
+    if constexpr (P::LOGN == 11) {
+        // pos bit 5 pairs lanes l, l^32: exchange halves, butterfly, keep the
+        // swapped arrangement (p1_addr accounts for it)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
+            r[2 * m] = pr[0];
+            r[2 * m + 1] = pr[1];
+            const uint2 wa = tw[32u + 2 * m];
+            const uint2 wb = tw[33u + 2 * m];
+            ct_bfly<P::Q>(r[2 * m], r[2 * m + 1], h ? wb.x : wa.x, h ? wb.y : wa.y);
+        }
+    }
+}
+
+// Per-lane pass-2 twiddles live in a per-workgroup LDS table, lane-major
+// (entry e, lane t) so a ds_read_b64 by 64 lanes is conflict-free:
+//   e = 2^(4-b) - 1 + m for stage bit b,  k = 2^(LOGN-1-b) + (Lp << (4-b)) + m
+constexpr int TW2_ENTRIES = 31;
+constexpr int TW2_WORDS = TW2_ENTRIES * 64 * 2;   // 15.5 KiB per direction
+
+__host__ __device__ constexpr int tw2_b(int e) { return e < 1 ? 4 : e < 3 ? 3 : e < 7 ? 2 : e < 15 ? 1 : 0; }
+
+template <int PS, bool INV, class P>
+__device__ __forceinline__ void fill_tw2(uint2 *tab)
+{
+    for (int i = threadIdx.x; i < TW2_ENTRIES * 64; i += blockDim.x) {
+        const int e = i >> 6, t = i & 63;
+        const int b = tw2_b(e);
+        const uint32_t m = e - ((1 << (4 - b)) - 1);
+        const uint32_t Lp = (P::LOGN == 11) ? (uint32_t)t : (uint32_t)(t & 31);
+        tab[i] = twd<PS, INV>((1u << (P::LOGN - 1 - b)) + (Lp << (4 - b)) + m);
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void fwd_pass2(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
+{
+#pragma unroll
+    for (int b = 4; b >= 0; --b) {
+        const int hh = 1 << b;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
+                const uint2 w = tab[e * 64 + lane];
+                ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+            }
+        }
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
+{
+#pragma unroll
+    for (int b = 0; b <= 4; ++b) {
+        const int hh = 1 << b;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
+                const uint2 w = tab[e * 64 + lane];
+                gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+            }
+        }
+    }
+}
+
+// inverse pass 1: (n=2048) GS on pos bit 5 + swap back, then GS stages on pos
+// bits LOGN-5 .. LOGN-1 (j bits 0..4); the last one carries the n^-1 scaling
+// (times S0 / S1 constants), output canonical.
+template <int PS, class P, uint32_t S0, uint32_t S1>
+__device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h)
+{
+    const uint2 *tw = tw_base<PS, true>();
+    if constexpr (P::LOGN == 11) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const uint2 wa = tw[32u + 2 * m];
+            const uint2 wb = tw[33u + 2 * m];
+            gs_bfly<P::Q>(r[2 * m], r[2 * m + 1], h ? wb.x : wa.x, h ? wb.y : wa.y);
+            const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
+            r[2 * m] = pr[0];
+            r[2 * m + 1] = pr[1];
+        }
+    }
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+        const int hh = 1 << jb;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const uint2 w = tw[(16u >> jb) + (uint32_t)(j >> (jb + 1))];
+                gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+            }
+        }
+    }
+    constexpr uint32_t S0P = cshoup(S0, P::Q), S1P = cshoup(S1, P::Q);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t x = r[j], y = r[j + 16];
+        const uint32_t s = x + y;              // [0,4q)
+        const uint32_t d = x - y + 2 * P::Q;   // (0,4q)
+        uint32_t a = shoup_mul<P::Q>(s, S0, S0P);
+        uint32_t b = shoup_mul<P::Q>(d, S1, S1P);
+        r[j] = umin(a, a - P::Q);
+        r[j + 16] = umin(b, b - P::Q);
+    }
+}
+
+__device__ __forceinline__ constexpr uint32_t brv5(int j)
+{
+    return (uint32_t)(((j & 1) << 4) | ((j & 2) << 2) | (j & 4) | ((j & 8) >> 2) | ((j & 16) >> 4));
+}
+
+// ------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------
+// Workgroup = WGX waves, each with a private 8 KiB transpose buffer; the
+// lane-twiddle tables are shared by the workgroup.
+#ifndef NTT_WG
+#define NTT_WG 512          // fwd / inv: 8 waves, 64 + 15.5 KiB LDS -> 2 WG/CU
+#endif
+#ifndef MUL_WG
+#define MUL_WG 512          // poly_mul: 8 waves, 64 + 31 KiB LDS -> 1 WG/CU
+#endif
+#ifndef NTT_WAVES_PER_SIMD
+#define NTT_WAVES_PER_SIMD 4
+#endif
+#ifndef MUL_WAVES_PER_SIMD
+#define MUL_WAVES_PER_SIMD 2
+#endif
+constexpr int WG = 256;             // elementwise kernels
+
+template <int PS>
+__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const uint32_t *in, uint32_t *out, uint32_t npoly)
+{
+    using P = typename PSel<PS>::T;
+    using LT = Lane<P>;
+    constexpr uint32_t PPW = LT::BIG ? 1 : 2;
+    constexpr int WAVES = NTT_WG / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * 2048 + TW2_WORDS];
+    uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * 2048);
+    fill_tw2<PS, false, P>(tw2);
+    __syncthreads();
+    const LT L;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * 2048;
+
+    const uint32_t nunits = (npoly + PPW - 1) / PPW;
+    const uint32_t nw = gridDim.x * WAVES;
+    for (uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6); u < nunits; u += nw) {
+        const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
+        const bool valid = poly < npoly;
+        // per-lane base pointer + compile-time offsets (keeps the 32 addresses
+        // out of VGPRs: offsets fold into the instructions' immediate field)
+        const uint32_t *src = in + (size_t)poly * P::N + L.Lp;
+        uint32_t r[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) r[j] = valid ? src[LT::S * j] : 0u;
+        fwd_pass1<PS, P>(r, L.h);
+        lds_p1_to_p2<P>(r, buf, L);
+        fwd_pass2<P>(r, tw2, L.lane);
+        if (valid) {
+            uint32_t *dst = out + (size_t)poly * P::N + L.brl;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                uint32_t x = r[j];
+                x = umin(x, x - P::Q2);
+                x = umin(x, x - P::Q);
+                dst[brv5(j) * LT::S] = x;
+            }
+        }
+    }
+}
+
+template <int PS>
+__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const uint32_t *in, uint32_t *out, uint32_t npoly)
+{
+    using P = typename PSel<PS>::T;
+    using LT = Lane<P>;
+    constexpr uint32_t PPW = LT::BIG ? 1 : 2;
+    constexpr int WAVES = NTT_WG / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * 2048 + TW2_WORDS];
+    uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * 2048);
+    fill_tw2<PS, true, P>(tw2);
+    __syncthreads();
+    const LT L;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * 2048;
+
+    const uint32_t nunits = (npoly + PPW - 1) / PPW;
+    const uint32_t nw = gridDim.x * WAVES;
+    for (uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6); u < nunits; u += nw) {
+        const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
+        const bool valid = poly < npoly;
+        const uint32_t *src = in + (size_t)poly * P::N + L.brl;
+        uint32_t r[32];
+        // natural-order input; pass-2 position 32*Lp + j holds X[brv(pos)]
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const uint32_t x = valid ? src[brv5(j) * LT::S] : 0u;
+            r[j] = umin(x, x - P::Q2);   // tolerate inputs in [0, 4q)
+        }
+        inv_pass2<P>(r, tw2, L.lane);
+        lds_p2_to_p1<P>(r, buf, L);
+        inv_pass1<PS, P, P::NINV, P::C1>(r, L.h);
+        if (valid) {
+            uint32_t *dst = out + (size_t)poly * P::N + L.Lp;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) dst[LT::S * j] = r[j];
+        }
+    }
+}
+
+// fused c = a*b mod (x^n+1): FWD(a), FWD(b), Montgomery pointwise (the 2^-32
+// is folded into the inverse's final n^-1 scaling), INV -- one HBM read of a
+// and b, one write of c.
+template <int PS>
+__global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly)
+{
+    using P = typename PSel<PS>::T;
+    using LT = Lane<P>;
+    constexpr uint32_t PPW = LT::BIG ? 1 : 2;
+    constexpr int WAVES = MUL_WG / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * 2048 + 2 * TW2_WORDS];
+    uint2 *ftw2 = reinterpret_cast<uint2 *>(lds + WAVES * 2048);
+    uint2 *itw2 = ftw2 + TW2_ENTRIES * 64;
+    fill_tw2<PS, false, P>(ftw2);
+    fill_tw2<PS, true, P>(itw2);
+    __syncthreads();
+    const LT L;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * 2048;
+
+    const uint32_t nunits = (npoly + PPW - 1) / PPW;
+    const uint32_t nw = gridDim.x * WAVES;
+    for (uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6); u < nunits; u += nw) {
+        const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
+        const bool valid = poly < npoly;
+        const size_t off = (size_t)poly * P::N + L.Lp;
+        const uint32_t *pa = a + off, *pb = b + off;
+        uint32_t ra[32], rb[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            ra[j] = valid ? pa[LT::S * j] : 0u;
+            rb[j] = valid ? pb[LT::S * j] : 0u;
+        }
+        fwd_pass1<PS, P>(ra, L.h);
+        lds_p1_to_p2<P>(ra, buf, L);
+        fwd_pass2<P>(ra, ftw2, L.lane);
+        fwd_pass1<PS, P>(rb, L.h);
+        lds_p1_to_p2<P>(rb, buf, L);
+        fwd_pass2<P>(rb, ftw2, L.lane);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const uint32_t x = umin(ra[j], ra[j] - P::Q2);
+            const uint32_t y = umin(rb[j], rb[j] - P::Q2);
+            ra[j] = mont_mul<P>(x, y);
+        }
+        inv_pass2<P>(ra, itw2, L.lane);
+        lds_p2_to_p1<P>(ra, buf, L);
+        inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h);
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) c[off + LT::S * j] = ra[j];
+        }
+    }
+}
+
+// c = a.*b mod q over `count` coefficients (count % 4 == 0): Montgomery then
+// Shoup by 2^32 mod q to undo the 2^-32.
+template <int PS>
+__global__ __launch_bounds__(WG) void k_pointwise(const uint4 *a, const uint4 *b, uint4 *c, size_t count4)
+{
+    using P = typename PSel<PS>::T;
+    constexpr uint32_t RP = cshoup(P::R, P::Q);
+    for (size_t i = (size_t)blockIdx.x * WG + threadIdx.x; i < count4; i += (size_t)gridDim.x * WG) {
+        const uint4 x = a[i], y = b[i];
+        uint32_t v[4] = {x.x, x.y, x.z, x.w}, w[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t m = mont_mul<P>(umin(v[k], v[k] - P::Q2), umin(w[k], w[k] - P::Q2));
+            m = shoup_mul<P::Q>(m, P::R, RP);
+            v[k] = umin(m, m - P::Q);
+        }
+        c[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(WG) void k_fill_uniform(uint32_t *x, size_t count, uint32_t q, uint64_t seed, uint64_t first)
+{
+    for (size_t i = (size_t)blockIdx.x * WG + threadIdx.x; i < count; i += (size_t)gridDim.x * WG) {
+        const uint64_t r = splitmix64(seed + (first + i + 1) * 0x9E3779B97F4A7C15ULL);
+        x[i] = (uint32_t)(((r >> 32) * (uint64_t)q) >> 32);
+    }
+}
+
+// ------------------------------------------------------------------------
+// host side: table upload, launch configuration, C ABI
+// ------------------------------------------------------------------------
+namespace {
+
+thread_local int t_last_hip = 0;
+
+constexpr int kMaxDev = 64;
+std::once_flag g_tab_once[kMaxDev];
+int g_tab_status[kMaxDev];
+std::once_flag g_cpu_tables_once;
+Tables g_cpu_tables[3];
+
+const Tables &cpu_tables(int ps)
+{
+    std::call_once(g_cpu_tables_once, [] {
+        for (int i = 0; i < 3; i++) make_tables(*param_set(i), g_cpu_tables[i]);
+    });
+    return g_cpu_tables[ps];
+}
+
+int upload_tables(int dev)
+{
+    struct Sym { const void *sym; int ps; bool inv; };
+    const Sym syms[6] = {{HIP_SYMBOL(c_fwd0), 0, false}, {HIP_SYMBOL(c_inv0), 0, true},
+                         {HIP_SYMBOL(c_fwd1), 1, false}, {HIP_SYMBOL(c_inv1), 1, true},
+                         {HIP_SYMBOL(c_fwd2), 2, false}, {HIP_SYMBOL(c_inv2), 2, true}};
+    for (const auto &s : syms) {
+        const Tables &t = cpu_tables(s.ps);
+        const std::vector<uint32_t> &v = s.inv ? t.inv : t.fwd;
+        hipError_t e = hipMemcpyToSymbol(s.sym, v.data(), v.size() * 4, 0, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { t_last_hip = (int)e; return NTT_ERR_HIP; }
+    }
+    (void)dev;
+    return NTT_OK;
+}
+
+int ensure_device_tables()
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) { t_last_hip = (int)e; return NTT_ERR_HIP; }
+    if (dev < 0 || dev >= kMaxDev) return NTT_ERR_HIP;
+    std::call_once(g_tab_once[dev], [dev] { g_tab_status[dev] = upload_tables(dev); });
+    return g_tab_status[dev];
+}
+
+struct DevInfo { int cus = 0; int occ[3][3] = {}; };
+DevInfo g_dev[kMaxDev];
+std::once_flag g_dev_once[kMaxDev];
+
+template <class K>
+int blocks_per_cu(K kernel, int wg)
+{
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, wg, 0) != hipSuccess || nb < 1) nb = 1;
+    return nb;
+}
+
+const DevInfo &dev_info()
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::call_once(g_dev_once[dev], [dev] {
+        DevInfo &d = g_dev[dev];
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) d.cus = prop.multiProcessorCount;
+        if (d.cus <= 0) d.cus = 256;
+        d.occ[0][0] = blocks_per_cu(k_ntt_fwd<0>, NTT_WG);
+        d.occ[0][1] = blocks_per_cu(k_ntt_fwd<1>, NTT_WG);
+        d.occ[0][2] = blocks_per_cu(k_ntt_fwd<2>, NTT_WG);
+        d.occ[1][0] = blocks_per_cu(k_ntt_inv<0>, NTT_WG);
+        d.occ[1][1] = blocks_per_cu(k_ntt_inv<1>, NTT_WG);
+        d.occ[1][2] = blocks_per_cu(k_ntt_inv<2>, NTT_WG);
+        d.occ[2][0] = blocks_per_cu(k_poly_mul<0>, MUL_WG);
+        d.occ[2][1] = blocks_per_cu(k_poly_mul<1>, MUL_WG);
+        d.occ[2][2] = blocks_per_cu(k_poly_mul<2>, MUL_WG);
+    });
+    return g_dev[dev];
+}
+
+// persistent grid: enough workgroups to fill every CU at the kernel's
+// occupancy, never more than there are 4-wave groups of work units
+uint32_t grid_for(int op, int ps, size_t npoly)
+{
+    const DevInfo &d = dev_info();
+    const size_t ppw = param_set(ps)->logn == 11 ? 1 : 2;
+    const size_t units = (npoly + ppw - 1) / ppw;
+    const size_t waves = (op == 2 ? MUL_WG : NTT_WG) / 64;
+    const size_t need = (units + waves - 1) / waves;
+    const size_t cap = (size_t)d.cus * (size_t)d.occ[op][ps];
+    return (uint32_t)(need < cap ? need : cap);
+}
+
+int check_common(int ps, const void *p, size_t batch)
+{
+    if (!param_set(ps)) return NTT_ERR_PARAM;
+    if (batch == 0) return NTT_OK;
+    if (!p) return NTT_ERR_NULL;
+    if (((uintptr_t)p) & 3u) return NTT_ERR_ALIGN;
+    if (batch > (size_t)0xFFFFFFFFu / 2) return NTT_ERR_SIZE;
+    return NTT_OK;
+}
+
+bool partial_overlap(const void *x, const void *y, size_t bytes)
+{
+    const uintptr_t a = (uintptr_t)x, b = (uintptr_t)y;
+    if (a == b) return false;
+    return a < b + bytes && b < a + bytes;
+}
+
+int finish_launch()
+{
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { t_last_hip = (int)e; return NTT_ERR_HIP; }
+    return NTT_OK;
+}
+
+template <template <int> class Launcher, class... Args>
+int dispatch(int ps, Args... args)
+{
+    switch (ps) {
+    case 0: return Launcher<0>::run(args...);
+    case 1: return Launcher<1>::run(args...);
+    case 2: return Launcher<2>::run(args...);
+    default: return NTT_ERR_PARAM;
+    }
+}
+
+template <int PS> struct LFwd {
+    static int run(const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s)
+    {
+        hipLaunchKernelGGL(k_ntt_fwd<PS>, dim3(grid_for(0, PS, batch)), dim3(NTT_WG), 0, s, in, out, (uint32_t)batch);
+        return finish_launch();
+    }
+};
+template <int PS> struct LInv {
+    static int run(const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s)
+    {
+        hipLaunchKernelGGL(k_ntt_inv<PS>, dim3(grid_for(1, PS, batch)), dim3(NTT_WG), 0, s, in, out, (uint32_t)batch);
+        return finish_launch();
+    }
+};
+template <int PS> struct LMul {
+    static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s)
+    {
+        hipLaunchKernelGGL(k_poly_mul<PS>, dim3(grid_for(2, PS, batch)), dim3(MUL_WG), 0, s, a, b, c, (uint32_t)batch);
+        return finish_launch();
+    }
+};
+template <int PS> struct LPw {
+    static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t count4, hipStream_t s)
+    {
+        const DevInfo &d = dev_info();
+        size_t g = (count4 + WG - 1) / WG, cap = (size_t)d.cus * 8;
+        hipLaunchKernelGGL(k_pointwise<PS>, dim3((uint32_t)(g < cap ? g : cap)), dim3(WG), 0, s,
+                           (const uint4 *)a, (const uint4 *)b, (uint4 *)c, count4);
+        return finish_launch();
+    }
+};
+
+int transform(bool inverse, uint32_t *out, const uint32_t *in, size_t batch, int ps, void *stream)
+{
+    int rc = check_common(ps, in, batch);
+    if (rc == NTT_OK && batch) rc = check_common(ps, out, batch);
+    if (rc != NTT_OK || batch == 0) return rc;
+    const size_t bytes = batch * param_set(ps)->n * 4;
+    if (partial_overlap(in, out, bytes)) return NTT_ERR_ALIAS;
+    if ((rc = ensure_device_tables()) != NTT_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    return inverse ? dispatch<LInv>(ps, in, out, batch, s) : dispatch<LFwd>(ps, in, out, batch, s);
+}
+
+}  // namespace
+}  // namespace qntt
+
+// ==========================================================================
+// C ABI (include/qtesla_ntt.h)
+// ==========================================================================
+using namespace qntt;
+
+extern "C" {
+
+int ntt_param_info(int ps, uint32_t *n, uint32_t *q, uint32_t *psi, uint32_t *omega,
+                   uint32_t *omega_inv, uint32_t *n_inv)
+{
+    const ParamSet *p = param_set(ps);
+    if (!p) return NTT_ERR_PARAM;
+    const Tables &t = cpu_tables(ps);
+    if (n) *n = p->n;
+    if (q) *q = p->q;
+    if (psi) *psi = p->psi;
+    if (omega) *omega = t.omega;
+    if (omega_inv) *omega_inv = t.omega_inv;
+    if (n_inv) *n_inv = t.n_inv;
+    return NTT_OK;
+}
+
+int ntt_get_tables(int ps, uint32_t *bitrev_tbl, uint32_t *Phi, uint32_t *invPhi, uint32_t *tf0, uint32_t *ti0)
+{
+    const ParamSet *p = param_set(ps);
+    if (!p) return NTT_ERR_PARAM;
+    const Tables &t = cpu_tables(ps);
+    const size_t b = (size_t)p->n * 4;
+    if (bitrev_tbl) memcpy(bitrev_tbl, t.bitrev_tbl.data(), b);
+    if (Phi) memcpy(Phi, t.Phi.data(), b);
+    if (invPhi) memcpy(invPhi, t.invPhi.data(), b);
+    if (tf0) memcpy(tf0, t.tf0.data(), b);
+    if (ti0) memcpy(ti0, t.ti0.data(), b);
+    return NTT_OK;
+}
+
+int poly_ntt(uint32_t *d_poly, const uint32_t *twiddleFactor, size_t batch, int ps, void *stream)
+{
+    (void)twiddleFactor;  // dead parameter, as in the reference kernels
+    return transform(false, d_poly, d_poly, batch, ps, stream);
+}
+
+int poly_invntt(uint32_t *d_poly, const uint32_t *twiddleFactor, size_t batch, int ps, void *stream)
+{
+    (void)twiddleFactor;
+    return transform(true, d_poly, d_poly, batch, ps, stream);
+}
+
+int poly_ntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch, int ps, void *stream)
+{
+    return transform(false, d_out, d_in, batch, ps, stream);
+}
+
+int poly_invntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch, int ps, void *stream)
+{
+    return transform(true, d_out, d_in, batch, ps, stream);
+}
+
+int poly_mul(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t batch, int ps, void *stream)
+{
+    int rc;
+    if ((rc = check_common(ps, d_a, batch)) != NTT_OK || batch == 0) return rc;
+    if ((rc = check_common(ps, d_b, batch)) != NTT_OK) return rc;
+    if ((rc = check_common(ps, d_c, batch)) != NTT_OK) return rc;
+    const size_t bytes = batch * param_set(ps)->n * 4;
+    if (partial_overlap(d_a, d_c, bytes) || partial_overlap(d_b, d_c, bytes)) return NTT_ERR_ALIAS;
+    if ((rc = ensure_device_tables()) != NTT_OK) return rc;
+    return dispatch<LMul>(ps, d_a, d_b, d_c, batch, (hipStream_t)stream);
+}
+
+int poly_pointwise(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t batch, int ps, void *stream)
+{
+    int rc;
+    if ((rc = check_common(ps, d_a, batch)) != NTT_OK || batch == 0) return rc;
+    if ((rc = check_common(ps, d_b, batch)) != NTT_OK) return rc;
+    if ((rc = check_common(ps, d_c, batch)) != NTT_OK) return rc;
+    if ((((uintptr_t)d_a) | ((uintptr_t)d_b) | ((uintptr_t)d_c)) & 15u) return NTT_ERR_ALIGN;
+    const size_t count = batch * param_set(ps)->n;
+    if (partial_overlap(d_a, d_c, count * 4) || partial_overlap(d_b, d_c, count * 4)) return NTT_ERR_ALIAS;
+    return dispatch<LPw>(ps, d_a, d_b, d_c, count / 4, (hipStream_t)stream);
+}
+
+int ntt_fill_uniform(uint32_t *d_poly, size_t batch, int ps, uint64_t seed, uint64_t first_poly, void *stream)
+{
+    int rc = check_common(ps, d_poly, batch);
+    if (rc != NTT_OK || batch == 0) return rc;
+    const ParamSet *p = param_set(ps);
+    const size_t count = batch * p->n;
+    const DevInfo &d = dev_info();
+    size_t g = (count + WG - 1) / WG, cap = (size_t)d.cus * 16;
+    hipLaunchKernelGGL(k_fill_uniform, dim3((uint32_t)(g < cap ? g : cap)), dim3(WG), 0, (hipStream_t)stream,
+                       d_poly, count, p->q, seed, first_poly * p->n);
+    return finish_launch();
+}
+
+int ntt_last_hip_error(void) { return t_last_hip; }
+
+const char *ntt_strerror(int code)
+{
+    switch (code) {
+    case NTT_OK: return "ok";
+    case NTT_ERR_PARAM: return "unknown param_set";
+    case NTT_ERR_NULL: return "NULL device pointer";
+    case NTT_ERR_ALIGN: return "misaligned device pointer";
+    case NTT_ERR_HIP: return "HIP runtime error";
+    case NTT_ERR_SIZE: return "batch too large";
+    case NTT_ERR_ALIAS: return "partially overlapping buffers";
+    default: return "unknown error";
+    }
+}
+
+int ntt_build_info(char *buf, size_t len)
+{
+    const char *s = "qtesla_ntt gfx950: 1 launch/op, wave-per-poly (n=2048) / half-wave-per-poly (n=1024), "
+                    "32 coeff/lane, LDS XOR-swizzled transpose, permlane32 bit-5 stage, Shoup/Harvey lazy butterflies";
+    if (!buf || !len) return (int)strlen(s);
+    snprintf(buf, len, "%s", s);
+    return (int)strlen(s);
+}
+
+}  // extern "C"

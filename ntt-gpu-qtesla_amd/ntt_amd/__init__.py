@@ -1,0 +1,217 @@
+"""ntt_amd -- Python host binding of the MI355X batched negacyclic NTT engine.
+
+Thin ctypes layer over the C ABI in include/qtesla_ntt.h (libqtesla_ntt.so,
+built in-tree for gfx950).  PyTorch is used only as plumbing: device memory
+(int32 tensors carry the uint32 coefficient bit patterns), the current HIP
+stream and torch.distributed.  There is no CPU fallback: if the HIP library
+is missing every call raises.
+
+Names and argument meaning follow the reference's GPU pipeline
+(benlwk/ntt-gpu-qTESLA NTT.cu):
+  poly_ntt      -- bit_reverse_copy_tbl_Phi_gpu + radix2NTT_gpu0/1 (NTT.cu:2388-2400)
+  poly_invntt   -- GS_radix2INTT_gpu0/2 + bit_reverse_copy_tbl_invPhi_gpu (:2415-2425)
+  poly_mul      -- the whole CT-GS poly-mul driver (test_NTT_CT_GS_nega_gpu, :2358)
+  poly_pointwise -- pointwise_mult (:1155-1160)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(ROOT_DIR, "lib", "libqtesla_ntt.so")
+HEADER_PATH = os.path.join(os.path.dirname(ROOT_DIR), "include", "qtesla_ntt.h")
+
+PARAM_SETS = {"ref": 0, "p-I": 1, "p-III": 2}
+
+NTT_OK = 0
+NTT_ERR_PARAM = -1
+NTT_ERR_NULL = -2
+NTT_ERR_ALIGN = -3
+NTT_ERR_HIP = -4
+NTT_ERR_SIZE = -5
+NTT_ERR_ALIAS = -6
+
+
+class NTTError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        self.code = code
+        msg = lib().ntt_strerror(code).decode()
+        if code == NTT_ERR_HIP:
+            msg += f" (hipError {lib().ntt_last_hip_error()})"
+        super().__init__(f"{where}: {msg} [{code}]")
+
+
+_lib = None
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+
+def lib():
+    """Load libqtesla_ntt.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"HIP library {LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.ntt_param_info.argtypes = [ctypes.c_int] + [_u32p] * 6
+        L.ntt_get_tables.argtypes = [ctypes.c_int] + [_u32p] * 5
+        for nm in ("poly_ntt", "poly_invntt"):
+            getattr(L, nm).argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
+        for nm in ("poly_ntt_oop", "poly_invntt_oop"):
+            getattr(L, nm).argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
+        for nm in ("poly_mul", "poly_pointwise"):
+            getattr(L, nm).argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, _vp]
+        L.ntt_fill_uniform.argtypes = [_vp, _sz, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp]
+        L.ntt_last_hip_error.restype = ctypes.c_int
+        L.ntt_strerror.restype = ctypes.c_char_p
+        L.ntt_strerror.argtypes = [ctypes.c_int]
+        L.ntt_build_info.argtypes = [ctypes.c_char_p, _sz]
+        _lib = L
+    return _lib
+
+
+def _ps(param_set) -> int:
+    return PARAM_SETS[param_set] if isinstance(param_set, str) else int(param_set)
+
+
+def _check(rc: int, where: str):
+    if rc != NTT_OK:
+        raise NTTError(rc, where)
+
+
+def param_info(param_set) -> dict:
+    vals = [ctypes.c_uint32() for _ in range(6)]
+    _check(lib().ntt_param_info(_ps(param_set), *[ctypes.byref(v) for v in vals]), "ntt_param_info")
+    return dict(zip(("n", "q", "psi", "omega", "omega_inv", "n_inv"), (v.value for v in vals)))
+
+
+def tables(param_set) -> dict:
+    n = param_info(param_set)["n"]
+    names = ("bitrev_tbl", "Phi", "invPhi", "tf0", "ti0")
+    out = {k: np.zeros(n, np.uint32) for k in names}
+    _check(lib().ntt_get_tables(_ps(param_set), *(out[k].ctypes.data_as(_u32p) for k in names)), "ntt_get_tables")
+    return out
+
+
+def build_info() -> str:
+    buf = ctypes.create_string_buffer(512)
+    lib().ntt_build_info(buf, 512)
+    return buf.value.decode()
+
+
+# ---------------------------------------------------------------- raw API
+# device pointers as ints, stream as int (hipStream_t) or None
+
+def raw_poly_ntt(ptr: int, batch: int, param_set, stream=None):
+    _check(lib().poly_ntt(ptr, None, batch, _ps(param_set), stream), "poly_ntt")
+
+
+def raw_poly_invntt(ptr: int, batch: int, param_set, stream=None):
+    _check(lib().poly_invntt(ptr, None, batch, _ps(param_set), stream), "poly_invntt")
+
+
+def raw_poly_mul(c: int, a: int, b: int, batch: int, param_set, stream=None):
+    _check(lib().poly_mul(c, a, b, batch, _ps(param_set), stream), "poly_mul")
+
+
+# ------------------------------------------------------------- torch API
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream(stream):
+    torch = _torch()
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+
+
+def _batch(t, n: int) -> int:
+    torch = _torch()
+    if not t.is_cuda:
+        raise ValueError("ntt_amd operates on device tensors only (no CPU fallback)")
+    if t.dtype not in (torch.int32, getattr(torch, "uint32", torch.int32)):
+        raise TypeError(f"expected int32/uint32 storage, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous (poly-major [batch][n])")
+    if t.numel() % n:
+        raise ValueError(f"numel {t.numel()} is not a multiple of n={n}")
+    return t.numel() // n
+
+
+def poly_ntt(t, param_set, stream=None):
+    """In-place forward negacyclic NTT of a [batch, n] device tensor."""
+    n = param_info(param_set)["n"]
+    _check(lib().poly_ntt(t.data_ptr(), None, _batch(t, n), _ps(param_set), _stream(stream)), "poly_ntt")
+    return t
+
+
+def poly_invntt(t, param_set, stream=None):
+    """In-place inverse negacyclic NTT (includes n^-1 and psi^-i)."""
+    n = param_info(param_set)["n"]
+    _check(lib().poly_invntt(t.data_ptr(), None, _batch(t, n), _ps(param_set), _stream(stream)), "poly_invntt")
+    return t
+
+
+def poly_ntt_oop(out, inp, param_set, stream=None):
+    n = param_info(param_set)["n"]
+    b = _batch(inp, n)
+    if _batch(out, n) != b:
+        raise ValueError("out/in batch mismatch")
+    _check(lib().poly_ntt_oop(out.data_ptr(), inp.data_ptr(), b, _ps(param_set), _stream(stream)), "poly_ntt_oop")
+    return out
+
+
+def poly_invntt_oop(out, inp, param_set, stream=None):
+    n = param_info(param_set)["n"]
+    b = _batch(inp, n)
+    if _batch(out, n) != b:
+        raise ValueError("out/in batch mismatch")
+    _check(lib().poly_invntt_oop(out.data_ptr(), inp.data_ptr(), b, _ps(param_set), _stream(stream)),
+           "poly_invntt_oop")
+    return out
+
+
+def poly_mul(c, a, b, param_set, stream=None):
+    """c = a*b mod (x^n + 1, q), fused single launch."""
+    n = param_info(param_set)["n"]
+    nb = _batch(a, n)
+    if _batch(b, n) != nb or _batch(c, n) != nb:
+        raise ValueError("batch mismatch")
+    _check(lib().poly_mul(c.data_ptr(), a.data_ptr(), b.data_ptr(), nb, _ps(param_set), _stream(stream)), "poly_mul")
+    return c
+
+
+def poly_pointwise(c, a, b, param_set, stream=None):
+    n = param_info(param_set)["n"]
+    nb = _batch(a, n)
+    if _batch(b, n) != nb or _batch(c, n) != nb:
+        raise ValueError("batch mismatch")
+    _check(lib().poly_pointwise(c.data_ptr(), a.data_ptr(), b.data_ptr(), nb, _ps(param_set), _stream(stream)),
+           "poly_pointwise")
+    return c
+
+
+def fill_uniform(t, param_set, seed: int, first_poly: int = 0, stream=None):
+    """Device-side counter-based uniform coefficients in [0, q)."""
+    n = param_info(param_set)["n"]
+    _check(lib().ntt_fill_uniform(t.data_ptr(), _batch(t, n), _ps(param_set), seed & (2**64 - 1), first_poly,
+                                  _stream(stream)), "ntt_fill_uniform")
+    return t
+
+
+def to_numpy_u32(t) -> np.ndarray:
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+def from_numpy_u32(a: np.ndarray, device="cuda"):
+    torch = _torch()
+    return torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32)).to(device)

