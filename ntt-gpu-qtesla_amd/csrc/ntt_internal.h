@@ -1,0 +1,13 @@
+// ntt_internal.h -- diagnostic entry points (not part of include/qtesla_ntt.h).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* op 0 = forward, 1 = inverse; variant 0 = full kernel, 1 = global load+store
+ * only, 2 = arithmetic only (no global memory), 3 = load + LDS transpose + store. */
+int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uint32_t *d_in, size_t batch, int ps, void *stream);
+#ifdef __cplusplus
+}
+#endif

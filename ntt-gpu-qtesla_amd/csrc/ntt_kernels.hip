@@ -33,6 +33,7 @@
 
 #include "../../include/qtesla_ntt.h"
 #include "params.hpp"
+#include "ntt_internal.h"
 
 namespace qntt {
 
@@ -112,13 +113,17 @@ __device__ __forceinline__ uint32_t shoup_mul(uint32_t a, uint32_t w, uint32_t w
     return a * w - qe * Q;
 }
 
-template <uint32_t Q>
-__device__ __forceinline__ void ct_bfly(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp)
+// Forward twiddles are stored NEGATED on the device (wn = 2^32 - w, Shoup
+// companion wp of w): the multiply-add then yields -t directly, so both outputs
+// cost one instruction each (v_sub, v_add3):  x' = a + t,  y' = a - t + 2q.
+template <uint32_t Q, bool REDUCE = true>
+__device__ __forceinline__ void ct_bfly(uint32_t &x, uint32_t &y, uint32_t wn, uint32_t wp)
 {
-    const uint32_t a = umin(x, x - 2 * Q);       // [0,4q) -> [0,2q)
-    const uint32_t t = shoup_mul<Q>(y, w, wp);   // [0,2q)
-    x = a + t;
-    y = a - t + 2 * Q;
+    const uint32_t a = REDUCE ? umin(x, x - 2 * Q) : x;        // [0,4q) -> [0,2q)
+    const uint32_t qe = __umulhi(y, wp);
+    const uint32_t tn = (uint32_t)((uint64_t)qe * Q + (uint32_t)(y * wn));   // -t, t in [0,2q)
+    x = a - tn;
+    y = a + tn + 2 * Q;
 }
 
 template <uint32_t Q>
@@ -252,7 +257,7 @@ __device__ __forceinline__ const uint2 *tw_base()
 // forward pass 1: CT stages on pos bits LOGN-1 .. LOGN-5 (j bits 4..0),
 // twiddle index k = 2^s + (j >> (5-s)) -- wave-uniform.
 template <int PS, class P>
-__device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h)
+__device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw)
 {
     const uint2 *tw = tw_base<PS, false>();
 #pragma unroll
@@ -262,7 +267,8 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h)
         for (int j = 0; j < 32; ++j) {
             if ((j & hh) == 0) {
                 const uint2 w = tw[(1u << s) + (uint32_t)(j >> (5 - s))];
-                ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+                if (s == 0) ct_bfly<P::Q, false>(r[j], r[j + hh], w.x, w.y);   // inputs < 2q
+                else ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
             }
         }
     }
@@ -274,9 +280,8 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h)
             const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
             r[2 * m] = pr[0];
             r[2 * m + 1] = pr[1];
-            const uint2 wa = tw[32u + 2 * m];
-            const uint2 wb = tw[33u + 2 * m];
-            ct_bfly<P::Q>(r[2 * m], r[2 * m + 1], h ? wb.x : wa.x, h ? wb.y : wa.y);
+            const uint2 w = sw[2 * m + h];    // k = 32 + 2m + h
+            ct_bfly<P::Q>(r[2 * m], r[2 * m + 1], w.x, w.y);
         }
     }
 }
@@ -285,7 +290,7 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h)
 // (entry e, lane t) so a ds_read_b64 by 64 lanes is conflict-free:
 //   e = 2^(4-b) - 1 + m for stage bit b,  k = 2^(LOGN-1-b) + (Lp << (4-b)) + m
 constexpr int TW2_ENTRIES = 31;
-constexpr int TW2_WORDS = TW2_ENTRIES * 64 * 2;   // 15.5 KiB per direction
+constexpr int TW2_WORDS = TW2_ENTRIES * 64 * 2 + 64;   // 15.5 KiB + the 32-entry bit-5 table
 
 __host__ __device__ constexpr int tw2_b(int e) { return e < 1 ? 4 : e < 3 ? 3 : e < 7 ? 2 : e < 15 ? 1 : 0; }
 
@@ -299,6 +304,8 @@ __device__ __forceinline__ void fill_tw2(uint2 *tab)
         const uint32_t Lp = (P::LOGN == 11) ? (uint32_t)t : (uint32_t)(t & 31);
         tab[i] = twd<PS, INV>((1u << (P::LOGN - 1 - b)) + (Lp << (4 - b)) + m);
     }
+    // bit-5 stage (n = 2048): entry 2m + h is k = 32 + 2m + h
+    if (threadIdx.x < 32) tab[TW2_ENTRIES * 64 + threadIdx.x] = twd<PS, INV>(32u + threadIdx.x);
 }
 
 template <class P>
@@ -339,15 +346,14 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
 // bits LOGN-5 .. LOGN-1 (j bits 0..4); the last one carries the n^-1 scaling
 // (times S0 / S1 constants), output canonical.
 template <int PS, class P, uint32_t S0, uint32_t S1>
-__device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h)
+__device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw)
 {
     const uint2 *tw = tw_base<PS, true>();
     if constexpr (P::LOGN == 11) {
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
-            const uint2 wa = tw[32u + 2 * m];
-            const uint2 wb = tw[33u + 2 * m];
-            gs_bfly<P::Q>(r[2 * m], r[2 * m + 1], h ? wb.x : wa.x, h ? wb.y : wa.y);
+            const uint2 w = sw[2 * m + h];
+            gs_bfly<P::Q>(r[2 * m], r[2 * m + 1], w.x, w.y);
             const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
             r[2 * m] = pr[0];
             r[2 * m + 1] = pr[1];
@@ -401,7 +407,45 @@ __device__ __forceinline__ constexpr uint32_t brv5(int j)
 #endif
 constexpr int WG = 256;             // elementwise kernels
 
-template <int PS>
+// Persistent loop over work units u0, u0+nw, ...  With NTT_PREFETCH the loop
+// is software-pipelined over two register sets: the loads of the wave's next
+// unit are in flight while the current one is transformed.
+#ifndef NTT_PREFETCH
+#define NTT_PREFETCH 0
+#endif
+template <class Load, class Process>
+__device__ __forceinline__ void persistent_loop(uint32_t u, uint32_t nunits, uint32_t nw, Load &load, Process &process)
+{
+    uint32_t ra[32];
+#if NTT_PREFETCH
+    uint32_t rb[32];
+    if (u < nunits) load(ra, u);
+    while (u < nunits) {
+        const uint32_t u1 = u + nw;
+        if (u1 < nunits) load(rb, u1);
+        process(ra, u);
+        if (u1 >= nunits) break;
+        const uint32_t u2 = u1 + nw;
+        if (u2 < nunits) load(ra, u2);
+        process(rb, u1);
+        u = u2;
+    }
+#else
+    for (; u < nunits; u += nw) {
+        load(ra, u);
+        process(ra, u);
+    }
+#endif
+}
+
+// V (diagnostic variants, reached only through ntt_debug_variant): 0 = full,
+// 1 = global load + store only, 2 = compute only (no global memory),
+// 3 = load + LDS transpose + store (no arithmetic)
+//
+// Persistent loop, software-pipelined over two register sets: the 32 loads of
+// the wave's next polynomial are in flight while the current one is
+// transformed, so HBM latency hides under the VALU work of the same wave.
+template <int PS, int V = 0>
 __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const uint32_t *in, uint32_t *out, uint32_t npoly)
 {
     using P = typename PSel<PS>::T;
@@ -414,35 +458,39 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     __syncthreads();
     const LT L;
     uint32_t *buf = lds + (threadIdx.x >> 6) * 2048;
-
     const uint32_t nunits = (npoly + PPW - 1) / PPW;
     const uint32_t nw = gridDim.x * WAVES;
-    for (uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6); u < nunits; u += nw) {
+
+    auto load = [&](uint32_t (&r)[32], uint32_t u) {
+        // per-lane base pointer + compile-time offsets (offsets fold into the
+        // instructions' immediate field instead of 32 address registers)
         const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
-        const bool valid = poly < npoly;
-        // per-lane base pointer + compile-time offsets (keeps the 32 addresses
-        // out of VGPRs: offsets fold into the instructions' immediate field)
+        const bool valid = LT::BIG || poly < npoly;
         const uint32_t *src = in + (size_t)poly * P::N + L.Lp;
-        uint32_t r[32];
 #pragma unroll
-        for (int j = 0; j < 32; ++j) r[j] = valid ? src[LT::S * j] : 0u;
-        fwd_pass1<PS, P>(r, L.h);
-        lds_p1_to_p2<P>(r, buf, L);
-        fwd_pass2<P>(r, tw2, L.lane);
-        if (valid) {
+        for (int j = 0; j < 32; ++j) r[j] = V == 2 ? L.lane * (j + u) : (valid ? src[LT::S * j] : 0u);
+    };
+    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+        const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
+        if constexpr (V == 0 || V == 2) fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        if constexpr (V != 1) lds_p1_to_p2<P>(r, buf, L);
+        if constexpr (V == 0 || V == 2) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        if (LT::BIG || poly < npoly) {
             uint32_t *dst = out + (size_t)poly * P::N + L.brl;
 #pragma unroll
             for (int j = 0; j < 32; ++j) {
                 uint32_t x = r[j];
                 x = umin(x, x - P::Q2);
                 x = umin(x, x - P::Q);
-                dst[brv5(j) * LT::S] = x;
+                if constexpr (V == 2) asm volatile("" ::"v"(x));
+                else dst[brv5(j) * LT::S] = x;
             }
         }
-    }
+    };
+    persistent_loop(blockIdx.x * WAVES + (threadIdx.x >> 6), nunits, nw, load, process);
 }
 
-template <int PS>
+template <int PS, int V = 0>
 __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const uint32_t *in, uint32_t *out, uint32_t npoly)
 {
     using P = typename PSel<PS>::T;
@@ -455,29 +503,33 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
     __syncthreads();
     const LT L;
     uint32_t *buf = lds + (threadIdx.x >> 6) * 2048;
-
     const uint32_t nunits = (npoly + PPW - 1) / PPW;
     const uint32_t nw = gridDim.x * WAVES;
-    for (uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6); u < nunits; u += nw) {
-        const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
-        const bool valid = poly < npoly;
-        const uint32_t *src = in + (size_t)poly * P::N + L.brl;
-        uint32_t r[32];
+
+    auto load = [&](uint32_t (&r)[32], uint32_t u) {
         // natural-order input; pass-2 position 32*Lp + j holds X[brv(pos)]
+        const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
+        const bool valid = LT::BIG || poly < npoly;
+        const uint32_t *src = in + (size_t)poly * P::N + L.brl;
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const uint32_t x = valid ? src[brv5(j) * LT::S] : 0u;
-            r[j] = umin(x, x - P::Q2);   // tolerate inputs in [0, 4q)
-        }
-        inv_pass2<P>(r, tw2, L.lane);
-        lds_p2_to_p1<P>(r, buf, L);
-        inv_pass1<PS, P, P::NINV, P::C1>(r, L.h);
-        if (valid) {
+        for (int j = 0; j < 32; ++j) r[j] = V == 2 ? L.lane * (j + u) : (valid ? src[brv5(j) * LT::S] : 0u);
+    };
+    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+        const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
+        // inputs < 2q by contract: they feed the GS butterflies directly
+        if constexpr (V == 0 || V == 2) inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        if constexpr (V != 1) lds_p2_to_p1<P>(r, buf, L);
+        if constexpr (V == 0 || V == 2) inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        if (LT::BIG || poly < npoly) {
             uint32_t *dst = out + (size_t)poly * P::N + L.Lp;
 #pragma unroll
-            for (int j = 0; j < 32; ++j) dst[LT::S * j] = r[j];
+            for (int j = 0; j < 32; ++j) {
+                if constexpr (V == 2) asm volatile("" ::"v"(r[j]));
+                else dst[LT::S * j] = r[j];
+            }
         }
-    }
+    };
+    persistent_loop(blockIdx.x * WAVES + (threadIdx.x >> 6), nunits, nw, load, process);
 }
 
 // fused c = a*b mod (x^n+1): FWD(a), FWD(b), Montgomery pointwise (the 2^-32
@@ -492,7 +544,7 @@ __global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const u
     constexpr int WAVES = MUL_WG / 64;
     __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * 2048 + 2 * TW2_WORDS];
     uint2 *ftw2 = reinterpret_cast<uint2 *>(lds + WAVES * 2048);
-    uint2 *itw2 = ftw2 + TW2_ENTRIES * 64;
+    uint2 *itw2 = ftw2 + TW2_WORDS / 2;
     fill_tw2<PS, false, P>(ftw2);
     fill_tw2<PS, true, P>(itw2);
     __syncthreads();
@@ -512,10 +564,10 @@ __global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const u
             ra[j] = valid ? pa[LT::S * j] : 0u;
             rb[j] = valid ? pb[LT::S * j] : 0u;
         }
-        fwd_pass1<PS, P>(ra, L.h);
+        fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64);
         lds_p1_to_p2<P>(ra, buf, L);
         fwd_pass2<P>(ra, ftw2, L.lane);
-        fwd_pass1<PS, P>(rb, L.h);
+        fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64);
         lds_p1_to_p2<P>(rb, buf, L);
         fwd_pass2<P>(rb, ftw2, L.lane);
 #pragma unroll
@@ -526,7 +578,7 @@ __global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const u
         }
         inv_pass2<P>(ra, itw2, L.lane);
         lds_p2_to_p1<P>(ra, buf, L);
-        inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h);
+        inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64);
         if (valid) {
 #pragma unroll
             for (int j = 0; j < 32; ++j) c[off + LT::S * j] = ra[j];
@@ -598,7 +650,9 @@ int upload_tables(int dev)
                          {HIP_SYMBOL(c_fwd2), 2, false}, {HIP_SYMBOL(c_inv2), 2, true}};
     for (const auto &s : syms) {
         const Tables &t = cpu_tables(s.ps);
-        const std::vector<uint32_t> &v = s.inv ? t.inv : t.fwd;
+        std::vector<uint32_t> v = s.inv ? t.inv : t.fwd;
+        if (!s.inv)   // device forward table holds (2^32 - w, w'): see ct_bfly
+            for (size_t k = 0; k < v.size(); k += 2) v[k] = 0u - v[k];
         hipError_t e = hipMemcpyToSymbol(s.sym, v.data(), v.size() * 4, 0, hipMemcpyHostToDevice);
         if (e != hipSuccess) { t_last_hip = (int)e; return NTT_ERR_HIP; }
     }
@@ -841,6 +895,38 @@ int ntt_fill_uniform(uint32_t *d_poly, size_t batch, int ps, uint64_t seed, uint
 }
 
 int ntt_last_hip_error(void) { return t_last_hip; }
+
+// Diagnostic entry point (csrc/ntt_internal.h, not part of the public ABI):
+// launches kernel variant `variant` of op 0 = forward / 1 = inverse with the
+// production grid, for bottleneck attribution (tools/variants.py).
+int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uint32_t *d_in, size_t batch, int ps, void *stream)
+{
+    int rc = check_common(ps, d_in, batch);
+    if (rc != NTT_OK || batch == 0) return rc;
+    if ((rc = ensure_device_tables()) != NTT_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t g = grid_for(op, ps, batch), nb = (uint32_t)batch;
+#define QNTT_VAR(PSV)                                                                                   \
+    if (ps == PSV) {                                                                                    \
+        switch (op * 4 + variant) {                                                                     \
+        case 0: hipLaunchKernelGGL((k_ntt_fwd<PSV, 0>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
+        case 1: hipLaunchKernelGGL((k_ntt_fwd<PSV, 1>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
+        case 2: hipLaunchKernelGGL((k_ntt_fwd<PSV, 2>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
+        case 3: hipLaunchKernelGGL((k_ntt_fwd<PSV, 3>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
+        case 4: hipLaunchKernelGGL((k_ntt_inv<PSV, 0>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
+        case 5: hipLaunchKernelGGL((k_ntt_inv<PSV, 1>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
+        case 6: hipLaunchKernelGGL((k_ntt_inv<PSV, 2>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
+        case 7: hipLaunchKernelGGL((k_ntt_inv<PSV, 3>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
+        default: return NTT_ERR_PARAM;                                                                  \
+        }                                                                                               \
+        return finish_launch();                                                                         \
+    }
+    QNTT_VAR(0)
+    QNTT_VAR(1)
+    QNTT_VAR(2)
+#undef QNTT_VAR
+    return NTT_ERR_PARAM;
+}
 
 const char *ntt_strerror(int code)
 {

@@ -22,7 +22,7 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(ROOT_DIR, "lib", "libqtesla_ntt.so")
+LIB_PATH = os.environ.get("NTT_AMD_LIB") or os.path.join(ROOT_DIR, "lib", "libqtesla_ntt.so")
 HEADER_PATH = os.path.join(os.path.dirname(ROOT_DIR), "include", "qtesla_ntt.h")
 
 PARAM_SETS = {"ref": 0, "p-I": 1, "p-III": 2}

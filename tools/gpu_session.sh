@@ -1,0 +1,36 @@
+#!/bin/bash
+# One GPU-box session: each step has its own time limit; a fault / abort /
+# timeout ends the session (no further GPU work in this call).
+set -u
+mkdir -p gpurun_out
+run() {
+    local name=$1 secs=$2; shift 2
+    echo "[$(date +%T)] start $name" | tee -a gpurun_out/session.log
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "[$(date +%T)] $name rc=$rc" | tee -a gpurun_out/session.log
+    case $rc in 124|137|134|139|135|136) echo "fatal rc=$rc in $name, stopping"; exit $rc;; esac
+    return 0
+}
+for step in "$@"; do
+    case $step in
+        valu)   run valu 60 ./ntt-gpu-qtesla_amd/bin/valu_rates ;;
+        smoke)  run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        pytest) run pytest 600 python -m pytest tests -x -q -m gpu ;;
+        pytestq) run pytest 600 python -m pytest tests -x -q -m "gpu and not slow" ;;
+        bench)  run bench 400 python bench.py --steps 10 --warmup 2 --cpu-seconds 8 ;;
+        benchq) run bench 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+        benchmul) run benchmul 300 python bench.py --op polymul --steps 10 --warmup 2 --no-cpu-baseline ;;
+        bench1k) run bench1k 300 python bench.py --op fwd --param p-I --batch 65536 --steps 20 --warmup 2 --no-cpu-baseline ;;
+        prof)   run prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+        variants) run variants 300 python tools/variants.py --rounds 5 ;;
+        variants1k) run variants1k 300 python tools/variants.py --param p-I --batch 1048576 --rounds 5 ;;
+        pmc) run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 tools/variants.py --only fwd_full,inv_full,torch_copy --rounds 2 &&
+             run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 tools/variants.py --only fwd_full,inv_full,torch_copy --rounds 2 &&
+             run pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sq -o run -- python3 tools/variants.py --only fwd_full,inv_full --rounds 2 ;;
+        ab) for f in ntt-gpu-qtesla_amd/lib/ab/*.so; do b=$(basename $f .so); NTT_AMD_LIB=$PWD/$f run ab_$b 200 python tools/variants.py --rounds 5 --only fwd_full,inv_full,fwd_alu,inv_alu,fwd_mem,inv_mem || exit 1; done ;;
+        cycles) run cycles 120 ./ntt-gpu-qtesla_amd/bin/valu_cycles ;;
+        clock) run pmc_clock 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/pmc_clock -o run -- python3 tools/variants.py --rounds 2 ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
