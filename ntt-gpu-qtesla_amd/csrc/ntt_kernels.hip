@@ -105,12 +105,55 @@ __device__ __forceinline__ uint2 twd(uint32_t k)
 // ------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
+// NTT_FAKE_MUL (diagnostic builds only, results are wrong): every mul-class
+// instruction is replaced 1:1 by a cheap VALU op with the same dependences,
+// to price the 32-bit multiplies inside the real kernels.
+#ifndef NTT_FAKE_MUL
+#define NTT_FAKE_MUL 0
+#endif
+// NTT_FAKE_TW (diagnostic builds only): twiddles are compile-time constants
+// instead of table loads, to price the twiddle fetches.
+#ifndef NTT_FAKE_TW
+#define NTT_FAKE_TW 0
+#endif
+__device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b)
+{
+#if NTT_FAKE_MUL
+    uint32_t r;
+    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return __umulhi(a, b);
+#endif
+}
+__device__ __forceinline__ uint32_t mullo32(uint32_t a, uint32_t b)
+{
+#if NTT_FAKE_MUL
+    uint32_t r;
+    asm volatile("v_or_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return a * b;
+#endif
+}
+// low word of a*b + c
+__device__ __forceinline__ uint32_t madlo32(uint32_t a, uint32_t b, uint32_t c)
+{
+#if NTT_FAKE_MUL
+    uint32_t r;
+    asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return (uint32_t)((uint64_t)a * b + c);
+#endif
+}
+
 template <uint32_t Q>
 __device__ __forceinline__ uint32_t shoup_mul(uint32_t a, uint32_t w, uint32_t wp)
 {
     // a < 2^32, w < q, wp = floor(w 2^32 / q)  ->  result == a*w mod q, in [0, 2q)
-    const uint32_t qe = __umulhi(a, wp);
-    return a * w - qe * Q;
+    const uint32_t qe = mulhi32(a, wp);
+    return madlo32(qe, 0u - Q, mullo32(a, w));
 }
 
 // Forward twiddles are stored NEGATED on the device (wn = 2^32 - w, Shoup
@@ -120,8 +163,8 @@ template <uint32_t Q, bool REDUCE = true>
 __device__ __forceinline__ void ct_bfly(uint32_t &x, uint32_t &y, uint32_t wn, uint32_t wp)
 {
     const uint32_t a = REDUCE ? umin(x, x - 2 * Q) : x;        // [0,4q) -> [0,2q)
-    const uint32_t qe = __umulhi(y, wp);
-    const uint32_t tn = (uint32_t)((uint64_t)qe * Q + (uint32_t)(y * wn));   // -t, t in [0,2q)
+    const uint32_t qe = mulhi32(y, wp);
+    const uint32_t tn = madlo32(qe, Q, mullo32(y, wn));   // -t, t in [0,2q)
     x = a - tn;
     y = a + tn + 2 * Q;
 }
@@ -157,6 +200,8 @@ struct Lane {
     uint32_t wlo, woff;   // pass-1 LDS write/read (b32) address parts
     uint32_t rbase, rxm;  // pass-2 LDS read/write (b128) address parts
     uint32_t brl;         // bit-reversal of Lp over LOGN-5 bits
+    // two-round (4 KiB) transpose, see lds2_* below
+    uint32_t l0, p1b, p2b, p2x;
 
     __device__ __forceinline__ Lane()
     {
@@ -168,6 +213,14 @@ struct Lane {
         rxm = (((Lp >> 1) & 1) << 2) | (((Lp >> 2) & 1) << 3) | ((Lp & 1) << 4);
         rbase = 32 * (Lp ^ ((Lp >> 3) & 1)) + (BIG ? 0u : 1024 * h);
         brl = __builtin_bitreverse32(Lp) >> (32 - (P::LOGN - 5));
+        l0 = lane & 1;
+        // pass-1 side: c = off + 32*R + 16*b + (k ^ (g(R) << 2)), R = pos >> 6,
+        // b = pos & 1 = l0, k = (pos >> 1) & 15 = (lane & 31) >> 1; the lane part
+        // of R (n = 2048: R = 2m + h) and of g (h) is folded in here
+        p1b = BIG ? ((32 * h + 16 * l0 + ((lane & 31) >> 1)) ^ (h << 3)) : (512 * h + 16 * l0 + ((lane & 31) >> 1));
+        // pass-2 side: R = Lp >> 1, g = Lp2 | ((Lp1 ^ Lp3) << 1)
+        p2b = (BIG ? 0u : 512 * h) + 32 * (Lp >> 1);
+        p2x = (((Lp >> 2) & 1) | ((((Lp >> 1) ^ (Lp >> 3)) & 1) << 1)) << 2;
     }
 };
 
@@ -195,6 +248,15 @@ __device__ __forceinline__ uint32_t p1_addr(const Lane<P> &L, int j)
 }
 
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+// In-kernel phase stamp (diagnostic variants V >= 4 only): s_memtime with its
+// lgkmcnt wait in one statement, fenced against scheduling.
+#define NTT_STAMP(var)                                                                  \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");     \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+    } while (0)
 
 // A wave-uniform zero the compiler cannot see through.  Adding it to the
 // index of a uniform twiddle load keeps that load an s_load inside the
@@ -239,6 +301,117 @@ __device__ __forceinline__ void lds_p2_to_p1(uint32_t (&r)[32], uint32_t *buf, c
     compiler_fence();
 }
 
+// Two-round transpose through a 4 KiB per-wave buffer (NTT_LDS_ROUNDS == 2).
+// Round 1 moves the half of the coefficients with pos bit 5 == pos bit 0,
+// round 2 the other half, so a buffer of n/2 words suffices and eight waves
+// per SIMD fit in LDS.  That half is a per-lane register subset on both sides
+// (register pair 2m + l0 on the pass-1 side, j' = 2k + Lp0 on the pass-2
+// side): a per-lane pair swap (v_cndmask) before and after.  Compacted
+// index of a coefficient: c = 32*R + 16*b + (k ^ (g(R) << 2)) with R = pos>>6,
+// b = pos & 1, k = (pos >> 1) & 15 (bit 5 is implied by the round) and the
+// XOR swizzle g(R) = R1 | ((R0 ^ R2) << 1): conflict-free for ds_write_b32 /
+// ds_read_b32 on the pass-1 side and ds_read_b128 / ds_write_b128 on the
+// pass-2 side (tests/test_lds_layout.py).
+template <class P>
+__device__ __forceinline__ uint32_t lds2_p1_addr(const Lane<P> &L, int m)
+{
+    if constexpr (P::LOGN == 11) {   // R = 2m + h: g = m0 | ((h ^ m1) << 1)
+        const uint32_t gx = ((uint32_t)(m & 1) << 2) | ((uint32_t)((m >> 1) & 1) << 3);
+        return (L.p1b ^ gx) + 64u * m;
+    } else {                          // R = m
+        const uint32_t gx = ((uint32_t)((m >> 1) & 1) << 2) | ((uint32_t)(((m >> 0) ^ (m >> 2)) & 1) << 3);
+        return (L.p1b ^ gx) + 32u * m;
+    }
+}
+template <class P>
+__device__ __forceinline__ uint32_t lds2_p2_addr(const Lane<P> &L, uint32_t b, int cc)
+{
+    return L.p2b + 16u * b + ((4u * cc) ^ L.p2x);
+}
+
+template <class P>
+__device__ __forceinline__ void lds2_p1_to_p2(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
+{
+    const bool o = L.l0 != 0;
+    uint32_t f[16], s[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        f[m] = o ? r[2 * m + 1] : r[2 * m];
+        s[m] = o ? r[2 * m] : r[2 * m + 1];
+    }
+#pragma unroll
+    for (int rnd = 0; rnd < 2; ++rnd) {
+        uint32_t (&v)[16] = rnd ? s : f;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) buf[lds2_p1_addr<P>(L, m)] = v[m];
+        compiler_fence();
+        const uint32_t b = L.l0 ^ (uint32_t)rnd;   // pass-2 side: Lp0 (BIG: Lp = lane)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const uint4 t = *reinterpret_cast<const uint4 *>(buf + lds2_p2_addr<P>(L, b, cc));
+            v[4 * cc + 0] = t.x;
+            v[4 * cc + 1] = t.y;
+            v[4 * cc + 2] = t.z;
+            v[4 * cc + 3] = t.w;
+        }
+        compiler_fence();
+    }
+    // f holds j' = 2k + Lp0, s holds j' = 2k + 1 - Lp0
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        r[2 * k] = o ? s[k] : f[k];
+        r[2 * k + 1] = o ? f[k] : s[k];
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void lds2_p2_to_p1(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
+{
+    const bool o = L.l0 != 0;
+    uint32_t f[16], s[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        f[k] = o ? r[2 * k + 1] : r[2 * k];
+        s[k] = o ? r[2 * k] : r[2 * k + 1];
+    }
+#pragma unroll
+    for (int rnd = 0; rnd < 2; ++rnd) {
+        uint32_t (&v)[16] = rnd ? s : f;
+        const uint32_t b = L.l0 ^ (uint32_t)rnd;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+            *reinterpret_cast<uint4 *>(buf + lds2_p2_addr<P>(L, b, cc)) =
+                make_uint4(v[4 * cc + 0], v[4 * cc + 1], v[4 * cc + 2], v[4 * cc + 3]);
+        compiler_fence();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = buf[lds2_p1_addr<P>(L, m)];
+        compiler_fence();
+    }
+    // f holds register 2m + l0 of the pass-1 layout, s register 2m + 1 - l0
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        r[2 * m] = o ? s[m] : f[m];
+        r[2 * m + 1] = o ? f[m] : s[m];
+    }
+}
+
+#ifndef NTT_LDS_ROUNDS
+#define NTT_LDS_ROUNDS 1
+#endif
+constexpr int XPOSE_WORDS = NTT_LDS_ROUNDS == 2 ? 1024 : 2048;   // per wave
+template <class P>
+__device__ __forceinline__ void xpose_p1_to_p2(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
+{
+    if constexpr (NTT_LDS_ROUNDS == 2) lds2_p1_to_p2<P>(r, buf, L);
+    else lds_p1_to_p2<P>(r, buf, L);
+}
+template <class P>
+__device__ __forceinline__ void xpose_p2_to_p1(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
+{
+    if constexpr (NTT_LDS_ROUNDS == 2) lds2_p2_to_p1<P>(r, buf, L);
+    else lds_p2_to_p1<P>(r, buf, L);
+}
+
 // ------------------------------------------------------------------------
 // transform passes
 // ------------------------------------------------------------------------
@@ -266,7 +439,7 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
             if ((j & hh) == 0) {
-                const uint2 w = tw[(1u << s) + (uint32_t)(j >> (5 - s))];
+                const uint2 w = NTT_FAKE_TW ? make_uint2(0u - 12345u * (j + 1), 777u * (j + 3)) : tw[(1u << s) + (uint32_t)(j >> (5 - s))];
                 if (s == 0) ct_bfly<P::Q, false>(r[j], r[j + hh], w.x, w.y);   // inputs < 2q
                 else ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
             }
@@ -280,7 +453,7 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
             const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
             r[2 * m] = pr[0];
             r[2 * m + 1] = pr[1];
-            const uint2 w = sw[2 * m + h];    // k = 32 + 2m + h
+            const uint2 w = NTT_FAKE_TW ? make_uint2(0u - 5u * (m + 1), 99u * (m + 1)) : sw[2 * m + h];    // k = 32 + 2m + h
             ct_bfly<P::Q>(r[2 * m], r[2 * m + 1], w.x, w.y);
         }
     }
@@ -294,18 +467,29 @@ constexpr int TW2_WORDS = TW2_ENTRIES * 64 * 2 + 64;   // 15.5 KiB + the 32-entr
 
 __host__ __device__ constexpr int tw2_b(int e) { return e < 1 ? 4 : e < 3 ? 3 : e < 7 ? 2 : e < 15 ? 1 : 0; }
 
-template <int PS, bool INV, class P>
+// Host-built images of the per-workgroup LDS twiddle table (lane-major
+// pass-2 entries + the 32-entry bit-5 table), one per (param set, direction):
+// the workgroup prologue is then one coalesced 16 KiB copy with one wait.
+constexpr int TW2_VEC4 = TW2_WORDS / 4;   // 1008 uint4
+__device__ uint4 g_tw2img[3][2][TW2_VEC4];
+
+template <int PS, bool INV, int NT>
 __device__ __forceinline__ void fill_tw2(uint2 *tab)
 {
-    for (int i = threadIdx.x; i < TW2_ENTRIES * 64; i += blockDim.x) {
-        const int e = i >> 6, t = i & 63;
-        const int b = tw2_b(e);
-        const uint32_t m = e - ((1 << (4 - b)) - 1);
-        const uint32_t Lp = (P::LOGN == 11) ? (uint32_t)t : (uint32_t)(t & 31);
-        tab[i] = twd<PS, INV>((1u << (P::LOGN - 1 - b)) + (Lp << (4 - b)) + m);
+    const uint4 *src = g_tw2img[PS][INV ? 1 : 0];
+    uint4 *dst = reinterpret_cast<uint4 *>(tab);
+    constexpr int ITER = (TW2_VEC4 + NT - 1) / NT;
+    uint4 v[ITER];
+#pragma unroll
+    for (int k = 0; k < ITER; ++k) {
+        const int i = threadIdx.x + k * NT;
+        if (i < TW2_VEC4) v[k] = src[i];
     }
-    // bit-5 stage (n = 2048): entry 2m + h is k = 32 + 2m + h
-    if (threadIdx.x < 32) tab[TW2_ENTRIES * 64 + threadIdx.x] = twd<PS, INV>(32u + threadIdx.x);
+#pragma unroll
+    for (int k = 0; k < ITER; ++k) {
+        const int i = threadIdx.x + k * NT;
+        if (i < TW2_VEC4) dst[i] = v[k];
+    }
 }
 
 template <class P>
@@ -318,7 +502,7 @@ __device__ __forceinline__ void fwd_pass2(uint32_t (&r)[32], const uint2 *tab, u
         for (int j = 0; j < 32; ++j) {
             if ((j & hh) == 0) {
                 const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
-                const uint2 w = tab[e * 64 + lane];
+                const uint2 w = NTT_FAKE_TW ? make_uint2(0u - 31u * (e + 1), 1234u * (e + 1)) : tab[e * 64 + lane];
                 ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
             }
         }
@@ -407,35 +591,28 @@ __device__ __forceinline__ constexpr uint32_t brv5(int j)
 #endif
 constexpr int WG = 256;             // elementwise kernels
 
-// Persistent loop over work units u0, u0+nw, ...  With NTT_PREFETCH the loop
-// is software-pipelined over two register sets: the loads of the wave's next
-// unit are in flight while the current one is transformed.
-#ifndef NTT_PREFETCH
-#define NTT_PREFETCH 0
+// Work distribution: workgroup b owns the contiguous unit range
+// [b*WAVES*PPW, (b+1)*WAVES*PPW); at step i its waves take consecutive units
+// b*WAVES*PPW + i*WAVES + wave.  Workgroups are dispatched in order, so the
+// units in flight chip-wide form a sliding contiguous window of HBM: measured
+// 5.9 TB/s for this access shape vs 5.4 TB/s for a persistent grid-stride
+// loop (tools/copy_bw.hip, profiles/r01/copybw.log).
+// units per wave: chosen per launch by launch_for (up to NTT_PPW_MAX) so that
+// large batches amortise the workgroup prologue and small ones fill the chip
+#ifndef NTT_PPW_MAX
+#define NTT_PPW_MAX 16
 #endif
-template <class Load, class Process>
-__device__ __forceinline__ void persistent_loop(uint32_t u, uint32_t nunits, uint32_t nw, Load &load, Process &process)
+template <int WAVES, class Load, class Process>
+__device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Load &load, Process &process)
 {
-    uint32_t ra[32];
-#if NTT_PREFETCH
-    uint32_t rb[32];
-    if (u < nunits) load(ra, u);
-    while (u < nunits) {
-        const uint32_t u1 = u + nw;
-        if (u1 < nunits) load(rb, u1);
-        process(ra, u);
-        if (u1 >= nunits) break;
-        const uint32_t u2 = u1 + nw;
-        if (u2 < nunits) load(ra, u2);
-        process(rb, u1);
-        u = u2;
+    uint32_t r[32];
+    uint32_t u = blockIdx.x * (WAVES * ppw) + (threadIdx.x >> 6);
+#pragma unroll 1
+    for (uint32_t i = 0; i < ppw; ++i, u += WAVES) {
+        if (u >= nunits) break;
+        load(r, u);
+        process(r, u);
     }
-#else
-    for (; u < nunits; u += nw) {
-        load(ra, u);
-        process(ra, u);
-    }
-#endif
 }
 
 // V (diagnostic variants, reached only through ntt_debug_variant): 0 = full,
@@ -446,20 +623,19 @@ __device__ __forceinline__ void persistent_loop(uint32_t u, uint32_t nunits, uin
 // the wave's next polynomial are in flight while the current one is
 // transformed, so HBM latency hides under the VALU work of the same wave.
 template <int PS, int V = 0>
-__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const uint32_t *in, uint32_t *out, uint32_t npoly)
+__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const uint32_t *in, uint32_t *out, uint32_t npoly, uint32_t ppw)
 {
     using P = typename PSel<PS>::T;
     using LT = Lane<P>;
     constexpr uint32_t PPW = LT::BIG ? 1 : 2;
     constexpr int WAVES = NTT_WG / 64;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * 2048 + TW2_WORDS];
-    uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * 2048);
-    fill_tw2<PS, false, P>(tw2);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + TW2_WORDS];
+    uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
+    fill_tw2<PS, false, NTT_WG>(tw2);
     __syncthreads();
     const LT L;
-    uint32_t *buf = lds + (threadIdx.x >> 6) * 2048;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint32_t nunits = (npoly + PPW - 1) / PPW;
-    const uint32_t nw = gridDim.x * WAVES;
 
     auto load = [&](uint32_t (&r)[32], uint32_t u) {
         // per-lane base pointer + compile-time offsets (offsets fold into the
@@ -468,13 +644,21 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
         const bool valid = LT::BIG || poly < npoly;
         const uint32_t *src = in + (size_t)poly * P::N + L.Lp;
 #pragma unroll
-        for (int j = 0; j < 32; ++j) r[j] = V == 2 ? L.lane * (j + u) : (valid ? src[LT::S * j] : 0u);
+        for (int j = 0; j < 32; ++j) r[j] = (V == 2 || V == 5) ? L.lane * (j + u) : (valid ? src[LT::S * j] : 0u);
     };
+    // V 4/5: V 0/2 with per-phase s_memtime stamps accumulated per wave
+    constexpr bool STAMPS = V >= 4;
+    constexpr bool ALU = V == 0 || V == 2 || V == 4 || V == 5;
+    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0}, ts[7];
     auto process = [&](uint32_t (&r)[32], uint32_t u) {
         const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
-        if constexpr (V == 0 || V == 2) fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
-        if constexpr (V != 1) lds_p1_to_p2<P>(r, buf, L);
-        if constexpr (V == 0 || V == 2) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        if constexpr (STAMPS) NTT_STAMP(ts[0]);
+        if constexpr (ALU) fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        if constexpr (STAMPS) NTT_STAMP(ts[1]);
+        if constexpr (V != 1) xpose_p1_to_p2<P>(r, buf, L);
+        if constexpr (STAMPS) NTT_STAMP(ts[2]);
+        if constexpr (ALU) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        if constexpr (STAMPS) NTT_STAMP(ts[3]);
         if (LT::BIG || poly < npoly) {
             uint32_t *dst = out + (size_t)poly * P::N + L.brl;
 #pragma unroll
@@ -482,29 +666,43 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
                 uint32_t x = r[j];
                 x = umin(x, x - P::Q2);
                 x = umin(x, x - P::Q);
-                if constexpr (V == 2) asm volatile("" ::"v"(x));
+                if constexpr (V == 2 || V == 5) asm volatile("" ::"v"(x));
+                else if constexpr (V != 4) dst[brv5(j) * LT::S] = x;
                 else dst[brv5(j) * LT::S] = x;
             }
         }
+        if constexpr (STAMPS) {
+            NTT_STAMP(ts[4]);
+            for (int i = 0; i < 4; i++) acc[i] += ts[i + 1] - ts[i];
+        }
     };
-    persistent_loop(blockIdx.x * WAVES + (threadIdx.x >> 6), nunits, nw, load, process);
+    unsigned long long t_begin = 0, t_end = 0;
+    if constexpr (STAMPS) NTT_STAMP(t_begin);
+    chunk_loop<WAVES>(nunits, ppw, load, process);
+    if constexpr (STAMPS) {
+        NTT_STAMP(t_end);
+        if (L.lane == 0) {   // diagnostic build: stamps go to the (garbage) output buffer
+            unsigned long long *o = reinterpret_cast<unsigned long long *>(out) + (blockIdx.x * WAVES + (threadIdx.x >> 6)) * 8;
+            for (int k = 0; k < 4; k++) o[k] = acc[k];
+            o[4] = t_end - t_begin;
+        }
+    }
 }
 
 template <int PS, int V = 0>
-__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const uint32_t *in, uint32_t *out, uint32_t npoly)
+__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const uint32_t *in, uint32_t *out, uint32_t npoly, uint32_t ppw)
 {
     using P = typename PSel<PS>::T;
     using LT = Lane<P>;
     constexpr uint32_t PPW = LT::BIG ? 1 : 2;
     constexpr int WAVES = NTT_WG / 64;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * 2048 + TW2_WORDS];
-    uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * 2048);
-    fill_tw2<PS, true, P>(tw2);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + TW2_WORDS];
+    uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
+    fill_tw2<PS, true, NTT_WG>(tw2);
     __syncthreads();
     const LT L;
-    uint32_t *buf = lds + (threadIdx.x >> 6) * 2048;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint32_t nunits = (npoly + PPW - 1) / PPW;
-    const uint32_t nw = gridDim.x * WAVES;
 
     auto load = [&](uint32_t (&r)[32], uint32_t u) {
         // natural-order input; pass-2 position 32*Lp + j holds X[brv(pos)]
@@ -518,7 +716,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
         const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
         // inputs < 2q by contract: they feed the GS butterflies directly
         if constexpr (V == 0 || V == 2) inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
-        if constexpr (V != 1) lds_p2_to_p1<P>(r, buf, L);
+        if constexpr (V != 1) xpose_p2_to_p1<P>(r, buf, L);
         if constexpr (V == 0 || V == 2) inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
         if (LT::BIG || poly < npoly) {
             uint32_t *dst = out + (size_t)poly * P::N + L.Lp;
@@ -529,31 +727,33 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
             }
         }
     };
-    persistent_loop(blockIdx.x * WAVES + (threadIdx.x >> 6), nunits, nw, load, process);
+    chunk_loop<WAVES>(nunits, ppw, load, process);
 }
 
 // fused c = a*b mod (x^n+1): FWD(a), FWD(b), Montgomery pointwise (the 2^-32
 // is folded into the inverse's final n^-1 scaling), INV -- one HBM read of a
 // and b, one write of c.
 template <int PS>
-__global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly)
+__global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
 {
     using P = typename PSel<PS>::T;
     using LT = Lane<P>;
     constexpr uint32_t PPW = LT::BIG ? 1 : 2;
     constexpr int WAVES = MUL_WG / 64;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * 2048 + 2 * TW2_WORDS];
-    uint2 *ftw2 = reinterpret_cast<uint2 *>(lds + WAVES * 2048);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + 2 * TW2_WORDS];
+    uint2 *ftw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
     uint2 *itw2 = ftw2 + TW2_WORDS / 2;
-    fill_tw2<PS, false, P>(ftw2);
-    fill_tw2<PS, true, P>(itw2);
+    fill_tw2<PS, false, MUL_WG>(ftw2);
+    fill_tw2<PS, true, MUL_WG>(itw2);
     __syncthreads();
     const LT L;
-    uint32_t *buf = lds + (threadIdx.x >> 6) * 2048;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
 
     const uint32_t nunits = (npoly + PPW - 1) / PPW;
-    const uint32_t nw = gridDim.x * WAVES;
-    for (uint32_t u = blockIdx.x * WAVES + (threadIdx.x >> 6); u < nunits; u += nw) {
+    uint32_t u = blockIdx.x * (WAVES * ppw) + (threadIdx.x >> 6);
+#pragma unroll 1
+    for (uint32_t it = 0; it < ppw; ++it, u += WAVES) {   // dispatch-ordered chunk (see chunk_loop)
+        if (u >= nunits) break;
         const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
         const bool valid = poly < npoly;
         const size_t off = (size_t)poly * P::N + L.Lp;
@@ -565,10 +765,10 @@ __global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const u
             rb[j] = valid ? pb[LT::S * j] : 0u;
         }
         fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64);
-        lds_p1_to_p2<P>(ra, buf, L);
+        xpose_p1_to_p2<P>(ra, buf, L);
         fwd_pass2<P>(ra, ftw2, L.lane);
         fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64);
-        lds_p1_to_p2<P>(rb, buf, L);
+        xpose_p1_to_p2<P>(rb, buf, L);
         fwd_pass2<P>(rb, ftw2, L.lane);
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
@@ -577,7 +777,7 @@ __global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const u
             ra[j] = mont_mul<P>(x, y);
         }
         inv_pass2<P>(ra, itw2, L.lane);
-        lds_p2_to_p1<P>(ra, buf, L);
+        xpose_p2_to_p1<P>(ra, buf, L);
         inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64);
         if (valid) {
 #pragma unroll
@@ -603,6 +803,35 @@ __global__ __launch_bounds__(WG) void k_pointwise(const uint4 *a, const uint4 *b
             v[k] = umin(m, m - P::Q);
         }
         c[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// Diagnostic copy kernels (ntt_debug_variant op 2): one poly per wave,
+// persistent grid like the transforms; dword (the transforms' access shape)
+// vs dwordx4 accesses, to price access width against the HBM roofline.
+template <int W>
+__global__ __launch_bounds__(512) void k_copy_diag(const uint32_t *in, uint32_t *out, uint32_t npoly)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * 8;
+    for (uint32_t u = blockIdx.x * 8 + (threadIdx.x >> 6); u < npoly; u += nw) {
+        if constexpr (W == 4) {
+            const uint4 *s4 = reinterpret_cast<const uint4 *>(in + (size_t)u * 2048) + lane;
+            uint4 *d4 = reinterpret_cast<uint4 *>(out + (size_t)u * 2048) + lane;
+            uint4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = s4[64 * j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d4[64 * j] = v[j];
+        } else {
+            const uint32_t *s1 = in + (size_t)u * 2048 + lane;
+            uint32_t *d1 = out + (size_t)u * 2048 + lane;
+            uint32_t v[32];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) v[j] = s1[64 * j];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) d1[64 * j] = v[j];
+        }
     }
 }
 
@@ -656,6 +885,38 @@ int upload_tables(int dev)
         hipError_t e = hipMemcpyToSymbol(s.sym, v.data(), v.size() * 4, 0, hipMemcpyHostToDevice);
         if (e != hipSuccess) { t_last_hip = (int)e; return NTT_ERR_HIP; }
     }
+    // LDS twiddle-table images (see fill_tw2), in the device conventions
+    static std::vector<uint32_t> img[3][2];
+    static std::once_flag img_once;
+    std::call_once(img_once, [] {
+        for (int ps = 0; ps < 3; ps++)
+            for (int inv = 0; inv < 2; inv++) {
+                const ParamSet &p = *param_set(ps);
+                const Tables &t = cpu_tables(ps);
+                const std::vector<uint32_t> &tw = inv ? t.inv : t.fwd;
+                std::vector<uint32_t> &o = img[ps][inv];
+                o.assign(TW2_WORDS, 0);
+                auto put = [&](int slot, uint32_t k) {
+                    o[2 * slot] = inv ? tw[2 * k] : 0u - tw[2 * k];   // forward stored negated (ct_bfly)
+                    o[2 * slot + 1] = tw[2 * k + 1];
+                };
+                for (int e = 0; e < TW2_ENTRIES; e++) {
+                    const int b = e < 1 ? 4 : e < 3 ? 3 : e < 7 ? 2 : e < 15 ? 1 : 0;
+                    const uint32_t m = e - ((1u << (4 - b)) - 1);
+                    for (uint32_t lane = 0; lane < 64; lane++) {
+                        const uint32_t Lp = p.logn == 11 ? lane : (lane & 31);
+                        put(e * 64 + lane, (1u << (p.logn - 1 - b)) + (Lp << (4 - b)) + m);
+                    }
+                }
+                for (int i = 0; i < 32; i++) put(TW2_ENTRIES * 64 + i, 32u + i);   // bit-5 stage: k = 32 + 2m + h
+            }
+    });
+    for (int ps = 0; ps < 3; ps++)
+        for (int inv = 0; inv < 2; inv++) {
+            hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_tw2img), img[ps][inv].data(), TW2_WORDS * 4,
+                                             (size_t)(ps * 2 + inv) * TW2_WORDS * 4, hipMemcpyHostToDevice);
+            if (e != hipSuccess) { t_last_hip = (int)e; return NTT_ERR_HIP; }
+        }
     (void)dev;
     return NTT_OK;
 }
@@ -704,17 +965,19 @@ const DevInfo &dev_info()
     return g_dev[dev];
 }
 
-// persistent grid: enough workgroups to fill every CU at the kernel's
-// occupancy, never more than there are 4-wave groups of work units
-uint32_t grid_for(int op, int ps, size_t npoly)
+// Launch shape: one workgroup per `ppw * waves` consecutive work units.  ppw
+// grows with the batch (amortising the 16 KiB LDS-table prologue) but never
+// beyond what keeps >= 4 workgroups per CU in flight.
+struct Launch { uint32_t grid, ppw; };
+Launch launch_for(int op, int ps, size_t npoly)
 {
-    const DevInfo &d = dev_info();
-    const size_t ppw = param_set(ps)->logn == 11 ? 1 : 2;
-    const size_t units = (npoly + ppw - 1) / ppw;
-    const size_t waves = (op == 2 ? MUL_WG : NTT_WG) / 64;
-    const size_t need = (units + waves - 1) / waves;
-    const size_t cap = (size_t)d.cus * (size_t)d.occ[op][ps];
-    return (uint32_t)(need < cap ? need : cap);
+    const size_t upw = param_set(ps)->logn == 11 ? 1 : 2;
+    const size_t units = (npoly + upw - 1) / upw;
+    const size_t waves = (size_t)(op == 2 ? MUL_WG : NTT_WG) / 64;
+    const size_t min_groups = (size_t)dev_info().cus * 4;
+    size_t ppw = units / (waves * min_groups);
+    ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
+    return {(uint32_t)((units + waves * ppw - 1) / (waves * ppw)), (uint32_t)ppw};
 }
 
 int check_common(int ps, const void *p, size_t batch)
@@ -755,21 +1018,24 @@ int dispatch(int ps, Args... args)
 template <int PS> struct LFwd {
     static int run(const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s)
     {
-        hipLaunchKernelGGL(k_ntt_fwd<PS>, dim3(grid_for(0, PS, batch)), dim3(NTT_WG), 0, s, in, out, (uint32_t)batch);
+        const Launch l = launch_for(0, PS, batch);
+        hipLaunchKernelGGL(k_ntt_fwd<PS>, dim3(l.grid), dim3(NTT_WG), 0, s, in, out, (uint32_t)batch, l.ppw);
         return finish_launch();
     }
 };
 template <int PS> struct LInv {
     static int run(const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s)
     {
-        hipLaunchKernelGGL(k_ntt_inv<PS>, dim3(grid_for(1, PS, batch)), dim3(NTT_WG), 0, s, in, out, (uint32_t)batch);
+        const Launch l = launch_for(1, PS, batch);
+        hipLaunchKernelGGL(k_ntt_inv<PS>, dim3(l.grid), dim3(NTT_WG), 0, s, in, out, (uint32_t)batch, l.ppw);
         return finish_launch();
     }
 };
 template <int PS> struct LMul {
     static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s)
     {
-        hipLaunchKernelGGL(k_poly_mul<PS>, dim3(grid_for(2, PS, batch)), dim3(MUL_WG), 0, s, a, b, c, (uint32_t)batch);
+        const Launch l = launch_for(2, PS, batch);
+        hipLaunchKernelGGL(k_poly_mul<PS>, dim3(l.grid), dim3(MUL_WG), 0, s, a, b, c, (uint32_t)batch, l.ppw);
         return finish_launch();
     }
 };
@@ -905,18 +1171,27 @@ int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uint32_t *d_in
     if (rc != NTT_OK || batch == 0) return rc;
     if ((rc = ensure_device_tables()) != NTT_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
-    const uint32_t g = grid_for(op, ps, batch), nb = (uint32_t)batch;
+    if (op == 2) {   // copies of n = 2048 polys, 2 workgroups of 8 waves per CU
+        const uint32_t g2 = (uint32_t)dev_info().cus * 2;
+        if (variant == 0) hipLaunchKernelGGL((k_copy_diag<1>), dim3(g2), dim3(512), 0, s, d_in, d_out, (uint32_t)batch);
+        else hipLaunchKernelGGL((k_copy_diag<4>), dim3(g2), dim3(512), 0, s, d_in, d_out, (uint32_t)batch);
+        return finish_launch();
+    }
+    const Launch l = launch_for(op, ps, batch);
+    const uint32_t g = l.grid, nb = (uint32_t)batch, pw = l.ppw;
 #define QNTT_VAR(PSV)                                                                                   \
     if (ps == PSV) {                                                                                    \
-        switch (op * 4 + variant) {                                                                     \
-        case 0: hipLaunchKernelGGL((k_ntt_fwd<PSV, 0>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
-        case 1: hipLaunchKernelGGL((k_ntt_fwd<PSV, 1>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
-        case 2: hipLaunchKernelGGL((k_ntt_fwd<PSV, 2>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
-        case 3: hipLaunchKernelGGL((k_ntt_fwd<PSV, 3>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
-        case 4: hipLaunchKernelGGL((k_ntt_inv<PSV, 0>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
-        case 5: hipLaunchKernelGGL((k_ntt_inv<PSV, 1>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
-        case 6: hipLaunchKernelGGL((k_ntt_inv<PSV, 2>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
-        case 7: hipLaunchKernelGGL((k_ntt_inv<PSV, 3>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb); break; \
+        switch (op * 16 + variant) {                                                                     \
+        case 0: hipLaunchKernelGGL((k_ntt_fwd<PSV, 0>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
+        case 1: hipLaunchKernelGGL((k_ntt_fwd<PSV, 1>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
+        case 2: hipLaunchKernelGGL((k_ntt_fwd<PSV, 2>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
+        case 3: hipLaunchKernelGGL((k_ntt_fwd<PSV, 3>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
+        case 4: hipLaunchKernelGGL((k_ntt_fwd<PSV, 4>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
+        case 5: hipLaunchKernelGGL((k_ntt_fwd<PSV, 5>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
+        case 16: hipLaunchKernelGGL((k_ntt_inv<PSV, 0>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
+        case 17: hipLaunchKernelGGL((k_ntt_inv<PSV, 1>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
+        case 18: hipLaunchKernelGGL((k_ntt_inv<PSV, 2>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
+        case 19: hipLaunchKernelGGL((k_ntt_inv<PSV, 3>), dim3(g), dim3(NTT_WG), 0, s, d_in, d_out, nb, pw); break; \
         default: return NTT_ERR_PARAM;                                                                  \
         }                                                                                               \
         return finish_launch();                                                                         \

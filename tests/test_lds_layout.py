@@ -102,3 +102,89 @@ def test_bank_conflict_free(logn):
         a = [lanes[l].rbase + ((4 * c) ^ lanes[l].rxm) for l in range(64)]
         assert worst_conflict(a, G_B128_READ, lambda d: (d // 4) % 16, 1) == 1
         assert worst_conflict(a, G_B128_WRITE, lambda d: (d // 4) % 8, 1) == 1
+
+
+# ---------------- two-round 4 KiB transpose (NTT_LDS_ROUNDS == 2, default) --------------
+
+class Lane2(Lane):
+    def __init__(self, lane, logn):
+        super().__init__(lane, logn)
+        big = logn == 11
+        h, Lp = self.h, self.Lp
+        self.l0 = lane & 1
+        self.p1b = ((32 * h + 16 * self.l0 + ((lane & 31) >> 1)) ^ (h << 3)) if big else \
+            (512 * h + 16 * self.l0 + ((lane & 31) >> 1))
+        self.p2b = (0 if big else 512 * h) + 32 * (Lp >> 1)
+        self.p2x = (((Lp >> 2) & 1) | ((((Lp >> 1) ^ (Lp >> 3)) & 1) << 1)) << 2
+
+
+def lds2_p1_addr(L, m, logn):
+    if logn == 11:
+        gx = ((m & 1) << 2) | (((m >> 1) & 1) << 3)
+        return (L.p1b ^ gx) + 64 * m
+    gx = (((m >> 1) & 1) << 2) | ((((m >> 0) ^ (m >> 2)) & 1) << 3)
+    return (L.p1b ^ gx) + 32 * m
+
+
+def lds2_p2_addr(L, b, cc):
+    return L.p2b + 16 * b + ((4 * cc) ^ L.p2x)
+
+
+def compact(pos, half):
+    """reference compaction: c = 32 R + 16 b + (k ^ (g(R) << 2)), g(R) = R1 | (R0^R2) << 1"""
+    R, b, k = pos >> 6, pos & 1, (pos >> 1) & 15
+    g = ((R >> 1) & 1) | ((((R >> 0) ^ (R >> 2)) & 1) << 1)
+    return 512 * half + 32 * R + 16 * b + (k ^ (g << 2))
+
+
+@pytest.mark.parametrize("logn", [10, 11])
+def test_two_round_transpose_moves_every_coefficient(logn):
+    """Simulate both rounds: LDS contents written from the pass-1 registers and
+    read into pass-2 registers must deliver position 32*Lp + j' to register j'."""
+    lanes = [Lane2(l, logn) for l in range(64)]
+    p1 = {}   # (lane, j) -> (poly_half, pos)
+    for lane in range(64):
+        for j in range(32):
+            pos, poly = p1_pos(lane, j, logn)
+            p1[(lane, j)] = (poly, pos)
+    got = {}
+    for rnd in range(2):
+        mem = {}
+        for lane in range(64):
+            L = lanes[lane]
+            for m in range(16):
+                j = 2 * m + (L.l0 ^ rnd)              # f = r[2m + l0], s = r[2m + 1 - l0]
+                a = lds2_p1_addr(L, m, logn)
+                assert a not in mem or mem[a] is None
+                mem[a] = p1[(lane, j)]
+                poly, pos = p1[(lane, j)]
+                assert a == compact(pos, poly), (lane, m, rnd)
+                assert ((pos >> 5) & 1) ^ (pos & 1) == rnd
+        assert len(mem) == 1024                        # 4 KiB per wave
+        for lane in range(64):
+            L = lanes[lane]
+            b = L.l0 ^ rnd
+            for cc in range(4):
+                base = lds2_p2_addr(L, b, cc)
+                for i in range(4):
+                    k = 4 * cc + i
+                    jp = 2 * k + b                      # j' = 2k + Lp0 ^ rnd
+                    got[(lane, jp)] = mem[base + i]
+    for lane in range(64):
+        for jp in range(32):
+            Lp = lanes[lane].Lp
+            assert got[(lane, jp)] == (0 if logn == 11 else lane >> 5, 32 * Lp + jp)
+
+
+@pytest.mark.parametrize("logn", [10, 11])
+def test_two_round_bank_conflict_free(logn):
+    lanes = [Lane2(l, logn) for l in range(64)]
+    for m in range(16):
+        a = [lds2_p1_addr(lanes[l], m, logn) for l in range(64)]
+        assert worst_conflict(a, G_B32, lambda d: d % 32, 1) == 1
+    for rnd in range(2):
+        for cc in range(4):
+            a = [lds2_p2_addr(lanes[l], lanes[l].l0 ^ rnd, cc) for l in range(64)]
+            assert all(x % 4 == 0 for x in a)
+            assert worst_conflict(a, G_B128_READ, lambda d: (d // 4) % 16, 1) == 1
+            assert worst_conflict(a, G_B128_WRITE, lambda d: (d // 4) % 8, 1) == 1

@@ -31,6 +31,9 @@ for step in "$@"; do
         ab) for f in ntt-gpu-qtesla_amd/lib/ab/*.so; do b=$(basename $f .so); NTT_AMD_LIB=$PWD/$f run ab_$b 200 python tools/variants.py --rounds 5 --only fwd_full,inv_full,fwd_alu,inv_alu,fwd_mem,inv_mem || exit 1; done ;;
         cycles) run cycles 120 ./ntt-gpu-qtesla_amd/bin/valu_cycles ;;
         clock) run pmc_clock 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/pmc_clock -o run -- python3 tools/variants.py --rounds 2 ;;
+        bocc) run bocc 120 ./ntt-gpu-qtesla_amd/bin/bfly_occupancy ;;
+        stamps) run stamps 200 python tools/stamps.py ;;
+        copybw) run copybw 200 ./ntt-gpu-qtesla_amd/bin/copy_bw ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -38,6 +38,8 @@ def main():
     for op, opn in ((0, "fwd"), (1, "inv")):
         for v, vn in ((0, "full"), (1, "mem"), (2, "alu"), (3, "lds")):
             names[f"{opn}_{vn}"] = (op, v)
+    names["copy_dword"] = (2, 0)
+    names["copy_x4"] = (2, 1)
     todo = list(names) + ["torch_copy"]
     if args.only:
         todo = [t for t in todo if t in args.only.split(",")]
