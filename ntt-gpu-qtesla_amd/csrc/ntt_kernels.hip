@@ -189,6 +189,16 @@ __device__ __forceinline__ uint32_t mont_mul(uint32_t a, uint32_t b)
     return hi + __umulhi(m, P::Q) + (lo != 0u ? 1u : 0u);
 }
 
+// XOR swizzle of the wave-private transpose buffer (hi = pos >> 5):
+//   phys(pos) = pos ^ (pos8 << 2) ^ (pos9 << 3) ^ ((pos7 ^ pos10) << 4) ^ (pos7 << 5)
+// Bijective; conflict-free for ds_write_b32 / ds_read_b32 in the pass-1
+// layouts and ds_read_b128 / ds_write_b128 in the bit-reversed pass-2
+// layout (tests/test_lds_layout.py, gfx950 lane-group bank model).
+__host__ __device__ constexpr uint32_t xm_of(uint32_t hi)   // XOR on pos bits 2..4
+{
+    return (((hi >> 3) & 1) << 2) | (((hi >> 4) & 1) << 3) | ((((hi >> 2) ^ (hi >> 5)) & 1) << 4);
+}
+
 // ------------------------------------------------------------------------
 // per-lane geometry
 // ------------------------------------------------------------------------
@@ -199,40 +209,24 @@ struct Lane {
     uint32_t lane, h, Lp;
     uint32_t wlo, woff;   // pass-1 LDS write/read (b32) address parts
     uint32_t rbase, rxm;  // pass-2 LDS read/write (b128) address parts
-    uint32_t brl;         // bit-reversal of Lp over LOGN-5 bits
-    // two-round (4 KiB) transpose, see lds2_* below
-    uint32_t l0, p1b, p2b, p2x;
+    uint32_t brl;         // lane index within its poly: pass-1 column, and bitrev(Lp)
 
     __device__ __forceinline__ Lane()
     {
         lane = threadIdx.x & 63;
         h = lane >> 5;
-        Lp = BIG ? lane : (lane & 31);
-        wlo = (lane & 31) ^ (BIG ? (h << 2) : 0u);
+        // pass-2 row of this lane: Lp = bitrev(lane).  Then the bit-reversed
+        // side of each transform (forward store, inverse load) addresses
+        // brv5(j) * S + brv(Lp) = brv5(j) * S + lane: lane-contiguous 128/256-B runs.
+        Lp = BIG ? (__builtin_bitreverse32(lane) >> 26) : (__builtin_bitreverse32(lane & 31) >> 27);
+        wlo = lane & 31;
         woff = BIG ? 64 * h : 1024 * h;
-        rxm = (((Lp >> 1) & 1) << 2) | (((Lp >> 2) & 1) << 3) | ((Lp & 1) << 4);
-        rbase = 32 * (Lp ^ ((Lp >> 3) & 1)) + (BIG ? 0u : 1024 * h);
-        brl = __builtin_bitreverse32(Lp) >> (32 - (P::LOGN - 5));
-        l0 = lane & 1;
-        // pass-1 side: c = off + 32*R + 16*b + (k ^ (g(R) << 2)), R = pos >> 6,
-        // b = pos & 1 = l0, k = (pos >> 1) & 15 = (lane & 31) >> 1; the lane part
-        // of R (n = 2048: R = 2m + h) and of g (h) is folded in here
-        p1b = BIG ? ((32 * h + 16 * l0 + ((lane & 31) >> 1)) ^ (h << 3)) : (512 * h + 16 * l0 + ((lane & 31) >> 1));
-        // pass-2 side: R = Lp >> 1, g = Lp2 | ((Lp1 ^ Lp3) << 1)
-        p2b = (BIG ? 0u : 512 * h) + 32 * (Lp >> 1);
-        p2x = (((Lp >> 2) & 1) | ((((Lp >> 1) ^ (Lp >> 3)) & 1) << 1)) << 2;
+        rxm = xm_of(Lp);
+        rbase = 32 * (Lp ^ ((Lp >> 2) & 1)) + (BIG ? 0u : 1024 * h);
+        brl = BIG ? lane : (lane & 31);
     }
 };
 
-// XOR swizzle of the wave-private transpose buffer: phys(pos) =
-//   pos ^ (pos6<<2) ^ (pos7<<3) ^ (pos5<<4) ^ (pos8<<5)
-// (bijective; conflict-free for ds_write_b32/ds_read_b32 in the pass-1
-// layouts and ds_read_b128/ds_write_b128 in the pass-2 layout -- checked
-// by tests/test_lds_layout.py against the gfx950 lane-group bank model).
-__host__ __device__ constexpr uint32_t xm_of(uint32_t hi)
-{
-    return (((hi >> 1) & 1) << 2) | (((hi >> 2) & 1) << 3) | ((hi & 1) << 4);
-}
 // pos>>5 of register j in the pass-1 layout (n=2048: after the bit-5 swap)
 template <class P>
 __host__ __device__ constexpr uint32_t hi_of(int j)
@@ -243,8 +237,8 @@ __host__ __device__ constexpr uint32_t hi_of(int j)
 template <class P>
 __device__ __forceinline__ uint32_t p1_addr(const Lane<P> &L, int j)
 {
-    const uint32_t hj = hi_of<P>(j);
-    return (L.wlo ^ xm_of(hj)) + 32 * (hj ^ ((hj >> 3) & 1)) + L.woff;
+    const uint32_t hj = hi_of<P>(j);   // the lane part of hi (n = 2048: 2h) enters neither XOR term
+    return (L.wlo ^ xm_of(hj)) + 32 * (hj ^ ((hj >> 2) & 1)) + L.woff;
 }
 
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
@@ -301,115 +295,16 @@ __device__ __forceinline__ void lds_p2_to_p1(uint32_t (&r)[32], uint32_t *buf, c
     compiler_fence();
 }
 
-// Two-round transpose through a 4 KiB per-wave buffer (NTT_LDS_ROUNDS == 2).
-// Round 1 moves the half of the coefficients with pos bit 5 == pos bit 0,
-// round 2 the other half, so a buffer of n/2 words suffices and eight waves
-// per SIMD fit in LDS.  That half is a per-lane register subset on both sides
-// (register pair 2m + l0 on the pass-1 side, j' = 2k + Lp0 on the pass-2
-// side): a per-lane pair swap (v_cndmask) before and after.  Compacted
-// index of a coefficient: c = 32*R + 16*b + (k ^ (g(R) << 2)) with R = pos>>6,
-// b = pos & 1, k = (pos >> 1) & 15 (bit 5 is implied by the round) and the
-// XOR swizzle g(R) = R1 | ((R0 ^ R2) << 1): conflict-free for ds_write_b32 /
-// ds_read_b32 on the pass-1 side and ds_read_b128 / ds_write_b128 on the
-// pass-2 side (tests/test_lds_layout.py).
-template <class P>
-__device__ __forceinline__ uint32_t lds2_p1_addr(const Lane<P> &L, int m)
-{
-    if constexpr (P::LOGN == 11) {   // R = 2m + h: g = m0 | ((h ^ m1) << 1)
-        const uint32_t gx = ((uint32_t)(m & 1) << 2) | ((uint32_t)((m >> 1) & 1) << 3);
-        return (L.p1b ^ gx) + 64u * m;
-    } else {                          // R = m
-        const uint32_t gx = ((uint32_t)((m >> 1) & 1) << 2) | ((uint32_t)(((m >> 0) ^ (m >> 2)) & 1) << 3);
-        return (L.p1b ^ gx) + 32u * m;
-    }
-}
-template <class P>
-__device__ __forceinline__ uint32_t lds2_p2_addr(const Lane<P> &L, uint32_t b, int cc)
-{
-    return L.p2b + 16u * b + ((4u * cc) ^ L.p2x);
-}
-
-template <class P>
-__device__ __forceinline__ void lds2_p1_to_p2(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
-{
-    const bool o = L.l0 != 0;
-    uint32_t f[16], s[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        f[m] = o ? r[2 * m + 1] : r[2 * m];
-        s[m] = o ? r[2 * m] : r[2 * m + 1];
-    }
-#pragma unroll
-    for (int rnd = 0; rnd < 2; ++rnd) {
-        uint32_t (&v)[16] = rnd ? s : f;
-#pragma unroll
-        for (int m = 0; m < 16; ++m) buf[lds2_p1_addr<P>(L, m)] = v[m];
-        compiler_fence();
-        const uint32_t b = L.l0 ^ (uint32_t)rnd;   // pass-2 side: Lp0 (BIG: Lp = lane)
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-            const uint4 t = *reinterpret_cast<const uint4 *>(buf + lds2_p2_addr<P>(L, b, cc));
-            v[4 * cc + 0] = t.x;
-            v[4 * cc + 1] = t.y;
-            v[4 * cc + 2] = t.z;
-            v[4 * cc + 3] = t.w;
-        }
-        compiler_fence();
-    }
-    // f holds j' = 2k + Lp0, s holds j' = 2k + 1 - Lp0
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        r[2 * k] = o ? s[k] : f[k];
-        r[2 * k + 1] = o ? f[k] : s[k];
-    }
-}
-
-template <class P>
-__device__ __forceinline__ void lds2_p2_to_p1(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
-{
-    const bool o = L.l0 != 0;
-    uint32_t f[16], s[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        f[k] = o ? r[2 * k + 1] : r[2 * k];
-        s[k] = o ? r[2 * k] : r[2 * k + 1];
-    }
-#pragma unroll
-    for (int rnd = 0; rnd < 2; ++rnd) {
-        uint32_t (&v)[16] = rnd ? s : f;
-        const uint32_t b = L.l0 ^ (uint32_t)rnd;
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc)
-            *reinterpret_cast<uint4 *>(buf + lds2_p2_addr<P>(L, b, cc)) =
-                make_uint4(v[4 * cc + 0], v[4 * cc + 1], v[4 * cc + 2], v[4 * cc + 3]);
-        compiler_fence();
-#pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = buf[lds2_p1_addr<P>(L, m)];
-        compiler_fence();
-    }
-    // f holds register 2m + l0 of the pass-1 layout, s register 2m + 1 - l0
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        r[2 * m] = o ? s[m] : f[m];
-        r[2 * m + 1] = o ? f[m] : s[m];
-    }
-}
-
-#ifndef NTT_LDS_ROUNDS
-#define NTT_LDS_ROUNDS 1
-#endif
-constexpr int XPOSE_WORDS = NTT_LDS_ROUNDS == 2 ? 1024 : 2048;   // per wave
+constexpr int XPOSE_WORDS = 2048;   // per-wave transpose buffer (8 KiB)
 template <class P>
 __device__ __forceinline__ void xpose_p1_to_p2(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
 {
-    if constexpr (NTT_LDS_ROUNDS == 2) lds2_p1_to_p2<P>(r, buf, L);
-    else lds_p1_to_p2<P>(r, buf, L);
+    lds_p1_to_p2<P>(r, buf, L);
 }
 template <class P>
 __device__ __forceinline__ void xpose_p2_to_p1(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
 {
-    if constexpr (NTT_LDS_ROUNDS == 2) lds2_p2_to_p1<P>(r, buf, L);
-    else lds_p2_to_p1<P>(r, buf, L);
+    lds_p2_to_p1<P>(r, buf, L);
 }
 
 // ------------------------------------------------------------------------
@@ -642,7 +537,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
         // instructions' immediate field instead of 32 address registers)
         const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
         const bool valid = LT::BIG || poly < npoly;
-        const uint32_t *src = in + (size_t)poly * P::N + L.Lp;
+        const uint32_t *src = in + (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
 #pragma unroll
         for (int j = 0; j < 32; ++j) r[j] = (V == 2 || V == 5) ? L.lane * (j + u) : (valid ? src[LT::S * j] : 0u);
     };
@@ -719,7 +614,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
         if constexpr (V != 1) xpose_p2_to_p1<P>(r, buf, L);
         if constexpr (V == 0 || V == 2) inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
         if (LT::BIG || poly < npoly) {
-            uint32_t *dst = out + (size_t)poly * P::N + L.Lp;
+            uint32_t *dst = out + (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
 #pragma unroll
             for (int j = 0; j < 32; ++j) {
                 if constexpr (V == 2) asm volatile("" ::"v"(r[j]));
@@ -756,7 +651,7 @@ __global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const u
         if (u >= nunits) break;
         const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
         const bool valid = poly < npoly;
-        const size_t off = (size_t)poly * P::N + L.Lp;
+        const size_t off = (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
         const uint32_t *pa = a + off, *pb = b + off;
         uint32_t ra[32], rb[32];
 #pragma unroll
@@ -903,8 +798,8 @@ int upload_tables(int dev)
                 for (int e = 0; e < TW2_ENTRIES; e++) {
                     const int b = e < 1 ? 4 : e < 3 ? 3 : e < 7 ? 2 : e < 15 ? 1 : 0;
                     const uint32_t m = e - ((1u << (4 - b)) - 1);
-                    for (uint32_t lane = 0; lane < 64; lane++) {
-                        const uint32_t Lp = p.logn == 11 ? lane : (lane & 31);
+                    for (uint32_t lane = 0; lane < 64; lane++) {   // Lp = bitrev(lane), see Lane
+                        const uint32_t Lp = p.logn == 11 ? bitrev(lane, 6) : bitrev(lane & 31, 5);
                         put(e * 64 + lane, (1u << (p.logn - 1 - b)) + (Lp << (4 - b)) + m);
                     }
                 }

@@ -1,12 +1,13 @@
 """LDS transpose layout of ntt_kernels.hip, checked on the CPU.
 
 Mirrors the kernel's address formulas (Lane ctor, xm_of, hi_of, p1_addr,
-rbase/rxm) and checks: bijectivity, that each layout visits every
-coefficient once, 16-B alignment/contiguity of the b128 accesses, and zero
-bank conflicts under the gfx950 lane-group model of MI355X_MICROARCH.md
-(ds_write/read_b32: two 32-lane groups, bank = dword % 32; ds_read_b128: four
-16-lane groups, 16-B slot = (dword/4) % 16; ds_write_b128: eight 8-lane
-groups, slot = (dword/4) % 8).
+rbase/rxm) and checks: the swizzle is a bijection, every coefficient is
+moved to the right pass-2 register, 16-B alignment/contiguity of the b128
+accesses, zero bank conflicts under the gfx950 lane-group model of
+MI355X_MICROARCH.md (ds_write/read_b32: two 32-lane groups, bank = dword %
+32; ds_read_b128: four 16-lane groups, 16-B slot = (dword/4) % 16;
+ds_write_b128: eight 8-lane groups, slot = (dword/4) % 8), and that the
+bit-reversed side of each transform is lane-contiguous in HBM.
 """
 import pytest
 
@@ -17,20 +18,25 @@ G_B32 = [list(range(32)), list(range(32, 64))]
 G_B128_WRITE = [list(range(i, i + 8)) for i in range(0, 64, 8)]
 
 
+def brv(x, bits):
+    return int(format(x, f"0{bits}b")[::-1], 2) if bits else 0
+
+
 def xm_of(hi):
-    return (((hi >> 1) & 1) << 2) | (((hi >> 2) & 1) << 3) | ((hi & 1) << 4)
+    return (((hi >> 3) & 1) << 2) | (((hi >> 4) & 1) << 3) | ((((hi >> 2) ^ (hi >> 5)) & 1) << 4)
 
 
 class Lane:
     def __init__(self, lane, logn):
         big = logn == 11
+        self.lane = lane
         self.h = lane >> 5
-        self.Lp = lane if big else lane & 31
-        self.wlo = (lane & 31) ^ ((self.h << 2) if big else 0)
+        self.Lp = brv(lane, 6) if big else brv(lane & 31, 5)
+        self.wlo = lane & 31
         self.woff = 64 * self.h if big else 1024 * self.h
-        Lp = self.Lp
-        self.rxm = (((Lp >> 1) & 1) << 2) | (((Lp >> 2) & 1) << 3) | ((Lp & 1) << 4)
-        self.rbase = 32 * (Lp ^ ((Lp >> 3) & 1)) + (0 if big else 1024 * self.h)
+        self.rxm = xm_of(self.Lp)
+        self.rbase = 32 * (self.Lp ^ ((self.Lp >> 2) & 1)) + (0 if big else 1024 * self.h)
+        self.brl = lane if big else lane & 31
 
 
 def hi_of(j, logn):
@@ -39,7 +45,7 @@ def hi_of(j, logn):
 
 def p1_addr(L, j, logn):
     hj = hi_of(j, logn)
-    return (L.wlo ^ xm_of(hj)) + 32 * (hj ^ ((hj >> 3) & 1)) + L.woff
+    return (L.wlo ^ xm_of(hj)) + 32 * (hj ^ ((hj >> 2) & 1)) + L.woff
 
 
 def p1_pos(lane, j, logn):
@@ -50,7 +56,8 @@ def p1_pos(lane, j, logn):
 
 
 def phys(pos):
-    return pos ^ (((pos >> 6) & 1) << 2) ^ (((pos >> 7) & 1) << 3) ^ (((pos >> 5) & 1) << 4) ^ (((pos >> 8) & 1) << 5)
+    b = lambda i: (pos >> i) & 1  # noqa: E731
+    return pos ^ (b(8) << 2) ^ (b(9) << 3) ^ ((b(7) ^ b(10)) << 4) ^ (b(7) << 5)
 
 
 def worst_conflict(addrs, groups, bank_of, width):
@@ -74,18 +81,20 @@ def test_pass1_addresses_are_the_swizzle_of_the_position(logn):
 
 
 @pytest.mark.parametrize("logn", [10, 11])
-def test_pass2_addresses(logn):
-    seen = set()
+def test_transpose_delivers_every_coefficient(logn):
+    mem = {}
+    for lane in range(64):
+        L = Lane(lane, logn)
+        for j in range(32):
+            mem[p1_addr(L, j, logn)] = p1_pos(lane, j, logn)
+    assert len(mem) == 2048
     for lane in range(64):
         L = Lane(lane, logn)
         for c in range(8):
             a = L.rbase + ((4 * c) ^ L.rxm)
             assert a % 4 == 0
-            for i in range(4):
-                pos = 32 * L.Lp + 4 * c + i
-                assert a + i == phys(pos) + (0 if logn == 11 else 1024 * L.h)
-                seen.add(a + i)
-    assert seen == set(range(2048))
+            for i in range(4):   # register 4c+i of the pass-2 layout holds pos 32*Lp + 4c + i
+                assert mem[a + i] == (32 * L.Lp + 4 * c + i, 0 if logn == 11 else lane >> 5)
 
 
 def test_swizzle_bijective():
@@ -104,87 +113,13 @@ def test_bank_conflict_free(logn):
         assert worst_conflict(a, G_B128_WRITE, lambda d: (d // 4) % 8, 1) == 1
 
 
-# ---------------- two-round 4 KiB transpose (NTT_LDS_ROUNDS == 2, default) --------------
-
-class Lane2(Lane):
-    def __init__(self, lane, logn):
-        super().__init__(lane, logn)
-        big = logn == 11
-        h, Lp = self.h, self.Lp
-        self.l0 = lane & 1
-        self.p1b = ((32 * h + 16 * self.l0 + ((lane & 31) >> 1)) ^ (h << 3)) if big else \
-            (512 * h + 16 * self.l0 + ((lane & 31) >> 1))
-        self.p2b = (0 if big else 512 * h) + 32 * (Lp >> 1)
-        self.p2x = (((Lp >> 2) & 1) | ((((Lp >> 1) ^ (Lp >> 3)) & 1) << 1)) << 2
-
-
-def lds2_p1_addr(L, m, logn):
-    if logn == 11:
-        gx = ((m & 1) << 2) | (((m >> 1) & 1) << 3)
-        return (L.p1b ^ gx) + 64 * m
-    gx = (((m >> 1) & 1) << 2) | ((((m >> 0) ^ (m >> 2)) & 1) << 3)
-    return (L.p1b ^ gx) + 32 * m
-
-
-def lds2_p2_addr(L, b, cc):
-    return L.p2b + 16 * b + ((4 * cc) ^ L.p2x)
-
-
-def compact(pos, half):
-    """reference compaction: c = 32 R + 16 b + (k ^ (g(R) << 2)), g(R) = R1 | (R0^R2) << 1"""
-    R, b, k = pos >> 6, pos & 1, (pos >> 1) & 15
-    g = ((R >> 1) & 1) | ((((R >> 0) ^ (R >> 2)) & 1) << 1)
-    return 512 * half + 32 * R + 16 * b + (k ^ (g << 2))
-
-
 @pytest.mark.parametrize("logn", [10, 11])
-def test_two_round_transpose_moves_every_coefficient(logn):
-    """Simulate both rounds: LDS contents written from the pass-1 registers and
-    read into pass-2 registers must deliver position 32*Lp + j' to register j'."""
-    lanes = [Lane2(l, logn) for l in range(64)]
-    p1 = {}   # (lane, j) -> (poly_half, pos)
-    for lane in range(64):
-        for j in range(32):
-            pos, poly = p1_pos(lane, j, logn)
-            p1[(lane, j)] = (poly, pos)
-    got = {}
-    for rnd in range(2):
-        mem = {}
+def test_bitreversed_side_is_lane_contiguous(logn):
+    """forward store / inverse load address: natural index brv(32*Lp + j') = brv5(j')*S + brl"""
+    S = 64 if logn == 11 else 32
+    for j in range(32):
         for lane in range(64):
-            L = lanes[lane]
-            for m in range(16):
-                j = 2 * m + (L.l0 ^ rnd)              # f = r[2m + l0], s = r[2m + 1 - l0]
-                a = lds2_p1_addr(L, m, logn)
-                assert a not in mem or mem[a] is None
-                mem[a] = p1[(lane, j)]
-                poly, pos = p1[(lane, j)]
-                assert a == compact(pos, poly), (lane, m, rnd)
-                assert ((pos >> 5) & 1) ^ (pos & 1) == rnd
-        assert len(mem) == 1024                        # 4 KiB per wave
-        for lane in range(64):
-            L = lanes[lane]
-            b = L.l0 ^ rnd
-            for cc in range(4):
-                base = lds2_p2_addr(L, b, cc)
-                for i in range(4):
-                    k = 4 * cc + i
-                    jp = 2 * k + b                      # j' = 2k + Lp0 ^ rnd
-                    got[(lane, jp)] = mem[base + i]
-    for lane in range(64):
-        for jp in range(32):
-            Lp = lanes[lane].Lp
-            assert got[(lane, jp)] == (0 if logn == 11 else lane >> 5, 32 * Lp + jp)
-
-
-@pytest.mark.parametrize("logn", [10, 11])
-def test_two_round_bank_conflict_free(logn):
-    lanes = [Lane2(l, logn) for l in range(64)]
-    for m in range(16):
-        a = [lds2_p1_addr(lanes[l], m, logn) for l in range(64)]
-        assert worst_conflict(a, G_B32, lambda d: d % 32, 1) == 1
-    for rnd in range(2):
-        for cc in range(4):
-            a = [lds2_p2_addr(lanes[l], lanes[l].l0 ^ rnd, cc) for l in range(64)]
-            assert all(x % 4 == 0 for x in a)
-            assert worst_conflict(a, G_B128_READ, lambda d: (d // 4) % 16, 1) == 1
-            assert worst_conflict(a, G_B128_WRITE, lambda d: (d // 4) % 8, 1) == 1
+            L = Lane(lane, logn)
+            pos = 32 * L.Lp + j
+            assert brv(pos, logn) == brv(j, 5) * S + L.brl
+            assert L.brl == (lane if logn == 11 else lane & 31)

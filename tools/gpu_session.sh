@@ -34,6 +34,10 @@ for step in "$@"; do
         bocc) run bocc 120 ./ntt-gpu-qtesla_amd/bin/bfly_occupancy ;;
         stamps) run stamps 200 python tools/stamps.py ;;
         copybw) run copybw 200 ./ntt-gpu-qtesla_amd/bin/copy_bw ;;
+        pmcbench) run pmcb_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcb_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-check &&
+                  run pmcb_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcb_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-check &&
+                  run pmcb_sum 60 python3 tools/pmc_summary.py gpurun_out/pmcb_fetch/run_counter_collection.csv gpurun_out/pmcb_write/run_counter_collection.csv gpurun_out/pmc_summary.json ;;
+        profbench) run profbench 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profbench -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
