@@ -476,7 +476,7 @@ __device__ __forceinline__ constexpr uint32_t brv5(int j)
 #define NTT_WG 512          // fwd / inv: 8 waves, 64 + 15.5 KiB LDS -> 2 WG/CU
 #endif
 #ifndef MUL_WG
-#define MUL_WG 512          // poly_mul: 8 waves, 64 + 31 KiB LDS -> 1 WG/CU
+#define MUL_WG 512          // poly_mul: 8 waves, 64 + 31.5 KiB LDS -> 1 WG/CU (2 waves/SIMD beat 3-4: spills)
 #endif
 #ifndef NTT_WAVES_PER_SIMD
 #define NTT_WAVES_PER_SIMD 4
@@ -497,13 +497,22 @@ constexpr int WG = 256;             // elementwise kernels
 #ifndef NTT_PPW_MAX
 #define NTT_PPW_MAX 16
 #endif
-template <int WAVES, class Load, class Process>
-__device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Load &load, Process &process)
+// The first unit's global loads are issued before the workgroup prologue
+// (`prologue` = the LDS twiddle-table fill + barrier), so the fill latency
+// hides under the first unit's HBM latency.
+template <int WAVES, class Prologue, class Load, class Process>
+__device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prologue &prologue, Load &load,
+                                           Process &process)
 {
     uint32_t r[32];
     uint32_t u = blockIdx.x * (WAVES * ppw) + (threadIdx.x >> 6);
+    if (u < nunits) load(r, u);
+    prologue();   // every wave reaches the barrier inside
+    if (u >= nunits) return;
+    process(r, u);
 #pragma unroll 1
-    for (uint32_t i = 0; i < ppw; ++i, u += WAVES) {
+    for (uint32_t i = 1; i < ppw; ++i) {
+        u += WAVES;
         if (u >= nunits) break;
         load(r, u);
         process(r, u);
@@ -526,8 +535,10 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     constexpr int WAVES = NTT_WG / 64;
     __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + TW2_WORDS];
     uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
-    fill_tw2<PS, false, NTT_WG>(tw2);
-    __syncthreads();
+    auto prologue = [&]() {
+        fill_tw2<PS, false, NTT_WG>(tw2);
+        __syncthreads();
+    };
     const LT L;
     uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint32_t nunits = (npoly + PPW - 1) / PPW;
@@ -573,7 +584,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     };
     unsigned long long t_begin = 0, t_end = 0;
     if constexpr (STAMPS) NTT_STAMP(t_begin);
-    chunk_loop<WAVES>(nunits, ppw, load, process);
+    chunk_loop<WAVES>(nunits, ppw, prologue, load, process);
     if constexpr (STAMPS) {
         NTT_STAMP(t_end);
         if (L.lane == 0) {   // diagnostic build: stamps go to the (garbage) output buffer
@@ -593,8 +604,10 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
     constexpr int WAVES = NTT_WG / 64;
     __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + TW2_WORDS];
     uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
-    fill_tw2<PS, true, NTT_WG>(tw2);
-    __syncthreads();
+    auto prologue = [&]() {
+        fill_tw2<PS, true, NTT_WG>(tw2);
+        __syncthreads();
+    };
     const LT L;
     uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint32_t nunits = (npoly + PPW - 1) / PPW;
@@ -622,7 +635,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
             }
         }
     };
-    chunk_loop<WAVES>(nunits, ppw, load, process);
+    chunk_loop<WAVES>(nunits, ppw, prologue, load, process);
 }
 
 // fused c = a*b mod (x^n+1): FWD(a), FWD(b), Montgomery pointwise (the 2^-32
@@ -653,27 +666,27 @@ __global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const u
         const bool valid = poly < npoly;
         const size_t off = (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
         const uint32_t *pa = a + off, *pb = b + off;
+        // a first, then b: the transpose's memory fences keep b's loads below
+        // a's transform, so only ~64 coefficients are live at the peak
         uint32_t ra[32], rb[32];
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            ra[j] = valid ? pa[LT::S * j] : 0u;
-            rb[j] = valid ? pb[LT::S * j] : 0u;
-        }
-        fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64);
+        for (int j = 0; j < 32; ++j) ra[j] = valid ? pa[LT::S * j] : 0u;
+        fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
         xpose_p1_to_p2<P>(ra, buf, L);
-        fwd_pass2<P>(ra, ftw2, L.lane);
-        fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64);
-        xpose_p1_to_p2<P>(rb, buf, L);
-        fwd_pass2<P>(rb, ftw2, L.lane);
+        fwd_pass2<P>(ra, ftw2 + opaque_zero(), L.lane);
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
-            const uint32_t x = umin(ra[j], ra[j] - P::Q2);
-            const uint32_t y = umin(rb[j], rb[j] - P::Q2);
-            ra[j] = mont_mul<P>(x, y);
+            ra[j] = umin(ra[j], ra[j] - P::Q2);
+            rb[j] = valid ? pb[LT::S * j] : 0u;
         }
-        inv_pass2<P>(ra, itw2, L.lane);
+        fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+        xpose_p1_to_p2<P>(rb, buf, L);
+        fwd_pass2<P>(rb, ftw2 + opaque_zero(), L.lane);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(ra[j], umin(rb[j], rb[j] - P::Q2));
+        inv_pass2<P>(ra, itw2 + opaque_zero(), L.lane);
         xpose_p2_to_p1<P>(ra, buf, L);
-        inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64);
+        inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero());
         if (valid) {
 #pragma unroll
             for (int j = 0; j < 32; ++j) c[off + LT::S * j] = ra[j];
