@@ -111,7 +111,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--param", default="p-III")
     ap.add_argument("--batch", type=int, default=1 << 20, help="polynomials per GPU")
-    ap.add_argument("--op", default="fwdinv", choices=["fwdinv", "fwd", "inv", "polymul"])
+    ap.add_argument("--op", default="fwdinv", choices=["fwdinv", "fwd", "inv", "polymul", "nussbaumer"])
+    ap.add_argument("--ring", default="q", choices=["q", "m32"], help="--op nussbaumer: mod q or mod 2^32-1")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
@@ -136,7 +137,7 @@ def main():
     x = torch.empty(count * n, dtype=torch.int32, device=device)
     ntt_amd.fill_uniform(x, args.param, SEED, first)
     y = z = None
-    if args.op == "polymul":
+    if args.op in ("polymul", "nussbaumer"):
         y = torch.empty_like(x)
         z = torch.empty_like(x)
         ntt_amd.fill_uniform(y, args.param, SEED ^ 0xFFFF, first)
@@ -147,10 +148,13 @@ def main():
             ntt_amd.poly_ntt(x, args.param, stream)
         elif kind == "inv":
             ntt_amd.poly_invntt(x, args.param, stream)
-        else:
+        elif kind == "mul":
             ntt_amd.poly_mul(z, x, y, args.param, stream)
+        else:
+            ntt_amd.poly_mul_nussbaumer(z, x, y, args.param, args.ring, stream)
 
-    kinds = {"fwdinv": ["fwd", "inv"], "fwd": ["fwd"], "inv": ["inv"], "polymul": ["mul"]}[args.op]
+    kinds = {"fwdinv": ["fwd", "inv"], "fwd": ["fwd"], "inv": ["inv"], "polymul": ["mul"],
+             "nussbaumer": ["nus"]}[args.op]
 
     for _ in range(args.warmup):
         for k in kinds:
@@ -175,7 +179,7 @@ def main():
     per_kind = {k: sum(evs[s][i][0].elapsed_time(evs[s][i][1]) for s in range(args.steps)) / args.steps
                 for i, k in enumerate(kinds)}  # ms per launch
     dom = max(per_kind, key=per_kind.get)
-    bytes_per_coeff = 12 if dom == "mul" else 8
+    bytes_per_coeff = 12 if dom in ("mul", "nus") else 8
     alg_bytes = count * n * bytes_per_coeff
     achieved = alg_bytes / (per_kind[dom] * 1e-3) / 1e9
 
@@ -192,9 +196,11 @@ def main():
     units = world * count * args.steps
     value = units / elapsed
     workload = {"fwdinv": "fwd+inv negacyclic NTT", "fwd": "forward negacyclic NTT",
-                "inv": "inverse negacyclic NTT", "polymul": "fused negacyclic poly-mul"}[args.op]
+                "inv": "inverse negacyclic NTT", "polymul": "fused negacyclic poly-mul",
+                "nussbaumer": "Nussbaumer negacyclic product" + (" mod 2^32-1" if args.ring == "m32" else "")}[args.op]
     workload = f"{workload} n={n} qTESLA-{args.param}" if args.param != "ref" else f"{workload} n={n} ref q={pinfo['q']}"
-    unit = {"fwdinv": "fwd+inv pairs/s", "fwd": "NTTs/s", "inv": "INTTs/s", "polymul": "products/s"}[args.op]
+    unit = {"fwdinv": "fwd+inv pairs/s", "fwd": "NTTs/s", "inv": "INTTs/s", "polymul": "products/s",
+            "nussbaumer": "products/s"}[args.op]
     out = {
         "metric": METRIC if args.op == "fwdinv" and args.param == "p-III" else f"{unit} ({workload})",
         "value": value,

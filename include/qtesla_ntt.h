@@ -91,6 +91,21 @@ int poly_invntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch,
 int poly_mul(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,
              size_t batch, int param_set, void *stream);
 
+/* Nussbaumer negacyclic product (the paper's alternate algorithm): the
+ * reference's single-polynomial CPU routine nussbaumer_fft (NTT.cu:167-277,
+ * driver test_nussbaumer :1987-2005), batched on the GPU and extended from
+ * n = 1024 to n = param_set's n (1024 or 2048; split m = 32, r = n/32).
+ *   ring NTT_RING_M32: coefficients mod 2^32 - 1, the reference's ring
+ *                      (NTT.cu:102-134); any 32-bit input, 0xFFFFFFFF is
+ *                      read as zero, outputs canonical in [0, 2^32 - 1).
+ *   ring NTT_RING_Q:   coefficients mod param_set's q, inputs < 2q, outputs
+ *                      canonical -- bit-identical to poly_mul.
+ * d_c may alias d_a or d_b. */
+#define NTT_RING_Q 0
+#define NTT_RING_M32 1
+int poly_mul_nussbaumer(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,
+                        size_t batch, int param_set, int ring, void *stream);
+
 /* Pointwise product c[i] = a[i] * b[i] mod q over batch*n coefficients.
  * Replaces pointwise_mult (NTT.cu:1155-1160). */
 int poly_pointwise(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,

@@ -10,4 +10,9 @@ extern "C" {
 int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uint32_t *d_in, size_t batch, int ps, void *stream);
 #ifdef __cplusplus
 }
+namespace qntt {
+/* csrc/nussbaumer.hip: launches the Nussbaumer kernel; returns a hipError_t */
+int nussbaumer_launch(int ps, int ring, const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch,
+                      void *stream, int cus);
+}
 #endif

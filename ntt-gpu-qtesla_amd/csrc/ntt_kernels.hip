@@ -33,56 +33,11 @@
 
 #include "../../include/qtesla_ntt.h"
 #include "params.hpp"
+#include "pset.hpp"
 #include "ntt_internal.h"
 
 namespace qntt {
 
-// ------------------------------------------------------------------------
-// compile-time parameter sets
-// ------------------------------------------------------------------------
-constexpr uint32_t cpow(uint64_t b, uint64_t e, uint64_t q)
-{
-    uint64_t r = 1;
-    b %= q;
-    while (e) {
-        if (e & 1) r = r * b % q;
-        b = b * b % q;
-        e >>= 1;
-    }
-    return (uint32_t)r;
-}
-constexpr uint32_t cshoup(uint32_t w, uint32_t q) { return (uint32_t)(((uint64_t)w << 32) / q); }
-constexpr uint32_t cqinv_neg(uint32_t q)
-{
-    uint32_t inv = q;
-    for (int i = 0; i < 5; i++) inv *= 2u - q * inv;
-    return 0u - inv;
-}
-
-template <uint32_t Q_, int LOGN_, uint32_t PSI_>
-struct PSet {
-    static constexpr uint32_t Q = Q_;
-    static constexpr int LOGN = LOGN_;
-    static constexpr uint32_t N = 1u << LOGN_;
-    static constexpr uint32_t Q2 = 2 * Q_;
-    static constexpr uint32_t QNEG = cqinv_neg(Q_);
-    static constexpr uint32_t NINV = cpow(N, Q_ - 2, Q_);
-    static constexpr uint32_t PSI_INV = cpow(PSI_, Q_ - 2, Q_);
-    // inv twiddle of k = 1 is psi^-brv(1) = psi^-(n/2)
-    static constexpr uint32_t C1 = (uint32_t)((uint64_t)NINV * cpow(PSI_INV, N / 2, Q_) % Q_);
-    static constexpr uint32_t R = (uint32_t)((1ull << 32) % Q_);
-    static constexpr uint32_t NINV_R = (uint32_t)((uint64_t)NINV * R % Q_);
-    static constexpr uint32_t C1_R = (uint32_t)((uint64_t)C1 * R % Q_);
-};
-using PS0 = PSet<8404993u, 10, 2083362u>;
-using PS1 = PSet<343576577u, 10, cpow(3, (343576577u - 1) / 2048, 343576577u)>;
-using PS2 = PSet<856145921u, 11, cpow(3, (856145921u - 1) / 4096, 856145921u)>;
-static_assert(4ull * PS2::Q < (1ull << 32), "lazy bounds need 4q < 2^32");
-
-template <int PS> struct PSel;
-template <> struct PSel<0> { using T = PS0; };
-template <> struct PSel<1> { using T = PS1; };
-template <> struct PSel<2> { using T = PS2; };
 
 // twiddles (w, w'), index k in [0, n): fwd = psi^brv(k), inv = psi^-brv(k)
 __constant__ uint2 c_fwd0[1024];
@@ -1041,6 +996,23 @@ int poly_mul(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t bat
     if (partial_overlap(d_a, d_c, bytes) || partial_overlap(d_b, d_c, bytes)) return NTT_ERR_ALIAS;
     if ((rc = ensure_device_tables()) != NTT_OK) return rc;
     return dispatch<LMul>(ps, d_a, d_b, d_c, batch, (hipStream_t)stream);
+}
+
+int poly_mul_nussbaumer(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t batch, int ps, int ring,
+                        void *stream)
+{
+    int rc;
+    if ((rc = check_common(ps, d_a, batch)) != NTT_OK) return rc;
+    if (ring != NTT_RING_Q && ring != NTT_RING_M32) return NTT_ERR_PARAM;
+    if (batch == 0) return NTT_OK;
+    if ((rc = check_common(ps, d_b, batch)) != NTT_OK) return rc;
+    if ((rc = check_common(ps, d_c, batch)) != NTT_OK) return rc;
+    if ((((uintptr_t)d_a) | ((uintptr_t)d_b) | ((uintptr_t)d_c)) & 15u) return NTT_ERR_ALIGN;
+    const size_t bytes = batch * param_set(ps)->n * 4;
+    if (partial_overlap(d_a, d_c, bytes) || partial_overlap(d_b, d_c, bytes)) return NTT_ERR_ALIAS;
+    const int e = nussbaumer_launch(ps, ring, d_a, d_b, d_c, batch, stream, dev_info().cus);
+    if (e != (int)hipSuccess) { t_last_hip = e; return NTT_ERR_HIP; }
+    return NTT_OK;
 }
 
 int poly_pointwise(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t batch, int ps, void *stream)

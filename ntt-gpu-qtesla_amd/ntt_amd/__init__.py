@@ -12,6 +12,7 @@ Names and argument meaning follow the reference's GPU pipeline
   poly_invntt   -- GS_radix2INTT_gpu0/2 + bit_reverse_copy_tbl_invPhi_gpu (:2415-2425)
   poly_mul      -- the whole CT-GS poly-mul driver (test_NTT_CT_GS_nega_gpu, :2358)
   poly_pointwise -- pointwise_mult (:1155-1160)
+  poly_mul_nussbaumer -- nussbaumer_fft (:167-277), batched, n = 1024 / 2048
 """
 from __future__ import annotations
 
@@ -34,6 +35,8 @@ NTT_ERR_ALIGN = -3
 NTT_ERR_HIP = -4
 NTT_ERR_SIZE = -5
 NTT_ERR_ALIAS = -6
+
+RINGS = {"q": 0, "m32": 1}   # NTT_RING_Q, NTT_RING_M32
 
 
 class NTTError(RuntimeError):
@@ -67,6 +70,7 @@ def lib():
             getattr(L, nm).argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
         for nm in ("poly_mul", "poly_pointwise"):
             getattr(L, nm).argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, _vp]
+        L.poly_mul_nussbaumer.argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp]
         L.ntt_fill_uniform.argtypes = [_vp, _sz, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp]
         L.ntt_last_hip_error.restype = ctypes.c_int
         L.ntt_strerror.restype = ctypes.c_char_p
@@ -187,6 +191,21 @@ def poly_mul(c, a, b, param_set, stream=None):
     if _batch(b, n) != nb or _batch(c, n) != nb:
         raise ValueError("batch mismatch")
     _check(lib().poly_mul(c.data_ptr(), a.data_ptr(), b.data_ptr(), nb, _ps(param_set), _stream(stream)), "poly_mul")
+    return c
+
+
+def poly_mul_nussbaumer(c, a, b, param_set, ring="q", stream=None):
+    """c = a*b mod x^n + 1 by the Nussbaumer algorithm (nussbaumer_fft, NTT.cu:167-277).
+
+    ring "q": mod param_set's q (equals poly_mul); ring "m32": mod 2^32 - 1,
+    the reference's ring.  Buffers must be 16-byte aligned."""
+    n = param_info(param_set)["n"]
+    nb = _batch(a, n)
+    if _batch(b, n) != nb or _batch(c, n) != nb:
+        raise ValueError("batch mismatch")
+    r = RINGS[ring] if isinstance(ring, str) else int(ring)
+    _check(lib().poly_mul_nussbaumer(c.data_ptr(), a.data_ptr(), b.data_ptr(), nb, _ps(param_set), r,
+                                     _stream(stream)), "poly_mul_nussbaumer")
     return c
 
 

@@ -60,6 +60,10 @@ def lib():
         L.oracle_gpu_ct_gs_polymul.argtypes = [_u32p, _u32p, _u32p, ctypes.c_size_t, ctypes.c_int]
         L.oracle_gpu_ct_ct_polymul.argtypes = [_u32p, _u32p, _u32p, ctypes.c_size_t, ctypes.c_int]
         L.oracle_fill_uniform.argtypes = [_u32p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+        for nm in ("oracle_nussbaumer", "oracle_naive_negacyclic"):
+            getattr(L, nm).argtypes = [_u32p, _u32p, _u32p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_m32_canon.restype = ctypes.c_uint32
+        L.oracle_m32_canon.argtypes = [ctypes.c_uint32]
         L.oracle_time_fwd_inv.restype = ctypes.c_double
         L.oracle_time_fwd_inv.argtypes = [_u32p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         _lib = L
@@ -173,6 +177,47 @@ def time_fwd_inv(x: np.ndarray, param_set, threads: int = 1, reps: int = 1) -> f
     return lib().oracle_time_fwd_inv(_ptr(y), y.size // n, _ps(param_set), threads, reps)
 
 
+M32 = 0xFFFFFFFF   # the reference's Nussbaumer ring Z/(2^32-1) (NTT.cu:102-134)
+
+
+def _ring_q(ring, n):
+    """ring: "m32" (mod 2^32-1) or a param-set name / q (mod q)."""
+    if ring == "m32":
+        return 0
+    if isinstance(ring, str):
+        return params(ring)["q"]
+    return int(ring)
+
+
+def nussbaumer(x, y, n: int, ring="m32") -> np.ndarray:
+    """nussbaumer_fft (NTT.cu:167-277) restated, m=32, r=n/32, batched.
+
+    ring "m32": the reference's ones'-complement ring, op for op (so
+    0xFFFFFFFF can appear as a second zero; compare via m32_canon)."""
+    x = _batched(x, n)
+    y = _batched(y, n)
+    z = np.zeros_like(x)
+    rc = lib().oracle_nussbaumer(_ptr(z), _ptr(x), _ptr(y), x.size // n, n, _ring_q(ring, n))
+    assert rc == 0
+    return z.reshape(-1, n)
+
+
+def naive_negacyclic(x, y, n: int, ring="m32") -> np.ndarray:
+    """naive (NTT.cu:147-165) at full length n, batched."""
+    x = _batched(x, n)
+    y = _batched(y, n)
+    z = np.zeros_like(x)
+    rc = lib().oracle_naive_negacyclic(_ptr(z), _ptr(x), _ptr(y), x.size // n, n, _ring_q(ring, n))
+    assert rc == 0
+    return z.reshape(-1, n)
+
+
+def m32_canon(a) -> np.ndarray:
+    """canonical residue mod 2^32-1 (normalize, NTT.cu:125): 0xFFFFFFFF -> 0"""
+    a = np.asarray(a, np.uint32)
+    return np.where(a == np.uint32(M32), np.uint32(0), a)
+
+
 # ---------------- independent numpy definitions ----------------
 
 def ntt_direct_np(x: np.ndarray, param_set) -> np.ndarray:
@@ -192,6 +237,17 @@ def ntt_direct_np(x: np.ndarray, param_set) -> np.ndarray:
     for r in range(xs.shape[0]):
         out[r] = (((M * xs[r][None, :]) % q).sum(axis=1) % q).astype(np.uint32)
     return out.reshape(np.shape(x))
+
+
+def schoolbook_m32_np(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """a*b mod (x^n + 1, 2^32-1), one polynomial, exact Python-integer convolution."""
+    a = [int(v) for v in np.asarray(a, np.uint32)]
+    b = np.asarray(b, np.uint32).astype(object)
+    n = len(a)
+    full = np.convolve(np.array(a, dtype=object), b)
+    c = full[:n].copy()
+    c[: n - 1] -= full[n:]
+    return np.array([int(v) % M32 for v in c], dtype=np.uint32)
 
 
 def schoolbook_np(a: np.ndarray, b: np.ndarray, param_set) -> np.ndarray:

@@ -78,6 +78,24 @@ def make_vectors(ps: str) -> dict:
                 params=np.array([n, q, p["psi"], p["n_inv"]], np.uint64))
 
 
+def make_nussbaumer() -> dict:
+    """mod 2^32-1 operands over the full word range (0 and 0xFFFFFFFF included),
+    nussbaumer_fft restated (NTT.cu:167-277), canonical residues; each checked
+    against an exact big-integer schoolbook."""
+    rng = np.random.default_rng(0x4E55)
+    out = {}
+    for n in (1024, 2048):
+        x = rng.integers(0, 1 << 32, (2, n), dtype=np.uint64).astype(np.uint32)
+        y = rng.integers(0, 1 << 32, (2, n), dtype=np.uint64).astype(np.uint32)
+        x[0, :8] = O.M32
+        y[1, -8:] = 0
+        z = O.m32_canon(O.nussbaumer(x, y, n, "m32"))
+        for r in range(2):
+            assert np.array_equal(z[r], O.schoolbook_m32_np(x[r], y[r]))
+        out.update({f"x{n}": x, f"y{n}": y, f"z{n}": z})
+    return out
+
+
 def main():
     os.makedirs(HERE, exist_ok=True)
     if os.path.isdir(REF):
@@ -89,6 +107,8 @@ def main():
         v = make_vectors(ps)
         np.savez(os.path.join(HERE, f"vectors_{ps}.npz"), **v)
         print("wrote", f"vectors_{ps}.npz")
+    np.savez(os.path.join(HERE, "vectors_nussbaumer.npz"), **make_nussbaumer())
+    print("wrote vectors_nussbaumer.npz")
 
 
 if __name__ == "__main__":

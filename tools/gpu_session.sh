@@ -39,6 +39,10 @@ for step in "$@"; do
                   run pmcb_sum 60 python3 tools/pmc_summary.py gpurun_out/pmcb_fetch/run_counter_collection.csv gpurun_out/pmcb_write/run_counter_collection.csv gpurun_out/pmc_summary.json ;;
         profbench) run profbench 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profbench -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         abmul) for f in ntt-gpu-qtesla_amd/lib/ab/*.so; do b=$(basename $f .so); NTT_AMD_LIB=$PWD/$f run abmul_$b 200 python bench.py --op polymul --steps 5 --warmup 1 --no-cpu-baseline || exit 1; NTT_AMD_LIB=$PWD/$f run abmul1k_$b 200 python bench.py --op polymul --param p-I --steps 5 --warmup 1 --no-cpu-baseline || exit 1; done ;;
+        nustest) run nustest 400 python -m pytest tests/test_gpu_nussbaumer.py -x -q -m "gpu and not slow" ;;
+        nusbench) run nusbench_q 300 python bench.py --op nussbaumer --ring q --steps 5 --warmup 1 --no-cpu-baseline &&
+                  run nusbench_m32 300 python bench.py --op nussbaumer --ring m32 --steps 5 --warmup 1 --no-cpu-baseline &&
+                  run nusbench_q1k 300 python bench.py --op nussbaumer --ring q --param p-I --steps 5 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
