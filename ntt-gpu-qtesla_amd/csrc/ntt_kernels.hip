@@ -379,8 +379,15 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
 // inverse pass 1: (n=2048) GS on pos bit 5 + swap back, then GS stages on pos
 // bits LOGN-5 .. LOGN-1 (j bits 0..4); the last one carries the n^-1 scaling
 // (times S0 / S1 constants), output canonical.
-template <int PS, class P, uint32_t S0, uint32_t S1>
-__device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw)
+struct NoEmit {
+    __device__ __forceinline__ void operator()(int, uint32_t) const {}
+};
+
+// `emit(j, v)` is called with each final canonical output as soon as it is
+// computed (the inverse kernel stores from there, so its 32 stores interleave
+// with the last stage instead of queueing behind it as one tail).
+template <int PS, class P, uint32_t S0, uint32_t S1, class Emit = NoEmit>
+__device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw, const Emit &emit = Emit())
 {
     const uint2 *tw = tw_base<PS, true>();
     if constexpr (P::LOGN == 11) {
@@ -414,6 +421,8 @@ __device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const u
         uint32_t b = shoup_mul<P::Q>(d, S1, S1P);
         r[j] = umin(a, a - P::Q);
         r[j + 16] = umin(b, b - P::Q);
+        emit(j, r[j]);
+        emit(j + 16, r[j + 16]);
     }
 }
 
@@ -474,6 +483,99 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
     }
 }
 
+// ------------------------------------------------------------------------
+// LDS-DMA prefetch (NTT_DMA=1): the next unit's 8 KiB streams HBM -> LDS by
+// global_load_lds_dwordx4 into the wave's transpose buffer -- free from the
+// transpose read until the next unit's first ds_read -- while the current
+// unit's pass 2 and stores run.  No extra VGPRs (a register prefetch would
+// need 32 and cost a wave per SIMD), so HBM latency hides at the same
+// occupancy.  The DMA is inline asm (hipcc would otherwise wait vmcnt(0) --
+// i.e. for the previous unit's stores too -- before the buffer's ds_reads):
+// its completion is counted by hand.  vmcnt counts loads, stores and LDS-DMA
+// together in issue order (MI355X_MICROARCH.md), and exactly 32 stores follow
+// each DMA, so `s_waitcnt vmcnt(32)` retires precisely the DMA.
+// ------------------------------------------------------------------------
+#ifndef NTT_DMA
+#define NTT_DMA 0
+#endif
+
+// one 1 KiB piece: lane l's 16 B from gsrc -> LDS byte address lds + 16 l
+__device__ __forceinline__ void dma16(const uint32_t *gsrc, uint32_t lds)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds)
+                 : "memory");
+}
+
+// LDS byte address of a wave-uniform __shared__ pointer
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t *p)
+{
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)p);
+}
+
+// Unit u (2048 consecutive words: one n=2048 poly or two n=1024 polys) ->
+// the wave's buffer in natural order.  `pieces` = 8, or 4 when the unit's
+// second n=1024 poly lies past the batch.
+__device__ __forceinline__ void dma_unit(const uint32_t *unit, uint32_t lds, uint32_t lane, int pieces)
+{
+    const uint32_t *src = unit + 4 * lane;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        if (c < pieces) dma16(src + 256 * c, lds + 1024 * c);
+}
+
+// Output stores of the transforms; NTT_NT_STORE=1 marks them nontemporal
+// (streamed once, never re-read by the kernel).
+#ifndef NTT_NT_STORE
+#define NTT_NT_STORE 1
+#endif
+// NTT_INV_EMIT=1: the inverse stores each output from inside its last stage
+#ifndef NTT_INV_EMIT
+#define NTT_INV_EMIT 1
+#endif
+__device__ __forceinline__ void st_out(uint32_t *p, uint32_t v)
+{
+    if constexpr (NTT_NT_STORE) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+__device__ __forceinline__ void wait_vm(void) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_vm32(void) { asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); }
+__device__ __forceinline__ void wait_lgkm(void) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Work loop with the DMA prefetch: `read(r)` takes the unit from the buffer
+// into registers, `front(r, u)` runs up to and including the transpose (after
+// which the buffer is free), `back(r, u)` runs the rest and issues exactly 32
+// stores per lane.
+template <int WAVES, class Prologue, class Read, class Front, class Back>
+__device__ __forceinline__ void chunk_loop_dma(const uint32_t *in, uint32_t npoly, uint32_t nunits, uint32_t ppw,
+                                               uint32_t lds, uint32_t lane, bool half_units, Prologue &prologue,
+                                               Read &read, Front &front, Back &back)
+{
+    auto pieces = [&](uint32_t u) { return (half_units && 2 * u + 1 >= npoly) ? 4 : 8; };
+    uint32_t u = blockIdx.x * (WAVES * ppw) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (u < nunits) dma_unit(in + (size_t)u * 2048, lds, lane, pieces(u));
+    prologue();   // every wave reaches the barrier inside
+    if (u >= nunits) return;
+    wait_vm();
+    uint32_t r[32];
+#pragma unroll 1
+    for (uint32_t i = 0;; ++i) {
+        read(r);
+        front(r, u);
+        wait_lgkm();   // the transpose's reads are done: the buffer is free
+        const uint32_t un = u + WAVES;
+        const bool more = i + 1 < ppw && un < nunits;
+        if (more) dma_unit(in + (size_t)un * 2048, lds, lane, pieces(un));
+        back(r, u);
+        if (!more) break;
+        u = un;
+        wait_vm32();   // all but the 32 stores issued after the DMA
+    }
+}
+
 // V (diagnostic variants, reached only through ntt_debug_variant): 0 = full,
 // 1 = global load + store only, 2 = compute only (no global memory),
 // 3 = load + LDS transpose + store (no arithmetic)
@@ -511,15 +613,9 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     constexpr bool STAMPS = V >= 4;
     constexpr bool ALU = V == 0 || V == 2 || V == 4 || V == 5;
     unsigned long long acc[6] = {0, 0, 0, 0, 0, 0}, ts[7];
-    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+    // canonical output, bit-reversed registers -> natural order: brv5(j)*S + lane
+    auto store = [&](uint32_t (&r)[32], uint32_t u) {
         const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
-        if constexpr (STAMPS) NTT_STAMP(ts[0]);
-        if constexpr (ALU) fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
-        if constexpr (STAMPS) NTT_STAMP(ts[1]);
-        if constexpr (V != 1) xpose_p1_to_p2<P>(r, buf, L);
-        if constexpr (STAMPS) NTT_STAMP(ts[2]);
-        if constexpr (ALU) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
-        if constexpr (STAMPS) NTT_STAMP(ts[3]);
         if (LT::BIG || poly < npoly) {
             uint32_t *dst = out + (size_t)poly * P::N + L.brl;
 #pragma unroll
@@ -528,15 +624,41 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
                 x = umin(x, x - P::Q2);
                 x = umin(x, x - P::Q);
                 if constexpr (V == 2 || V == 5) asm volatile("" ::"v"(x));
-                else if constexpr (V != 4) dst[brv5(j) * LT::S] = x;
-                else dst[brv5(j) * LT::S] = x;
+                else st_out(dst + brv5(j) * LT::S, x);
             }
         }
+    };
+    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+        if constexpr (STAMPS) NTT_STAMP(ts[0]);
+        if constexpr (ALU) fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        if constexpr (STAMPS) NTT_STAMP(ts[1]);
+        if constexpr (V != 1) xpose_p1_to_p2<P>(r, buf, L);
+        if constexpr (STAMPS) NTT_STAMP(ts[2]);
+        if constexpr (ALU) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        if constexpr (STAMPS) NTT_STAMP(ts[3]);
+        store(r, u);
         if constexpr (STAMPS) {
             NTT_STAMP(ts[4]);
             for (int i = 0; i < 4; i++) acc[i] += ts[i + 1] - ts[i];
         }
     };
+    if constexpr (NTT_DMA && V == 0) {
+        const uint32_t *nb = buf + (LT::BIG ? 0u : 1024u * L.h) + L.brl;   // natural image, pass-1 layout
+        auto read = [&](uint32_t (&r)[32]) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) r[j] = nb[LT::S * j];
+        };
+        auto front = [&](uint32_t (&r)[32], uint32_t) {
+            fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+            xpose_p1_to_p2<P>(r, buf, L);
+        };
+        auto back = [&](uint32_t (&r)[32], uint32_t u) {
+            fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+            store(r, u);
+        };
+        chunk_loop_dma<WAVES>(in, npoly, nunits, ppw, lds_addr(buf), L.lane, !LT::BIG, prologue, read, front, back);
+        return;
+    }
     unsigned long long t_begin = 0, t_end = 0;
     if constexpr (STAMPS) NTT_STAMP(t_begin);
     chunk_loop<WAVES>(nunits, ppw, prologue, load, process);
@@ -575,21 +697,51 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
 #pragma unroll
         for (int j = 0; j < 32; ++j) r[j] = V == 2 ? L.lane * (j + u) : (valid ? src[brv5(j) * LT::S] : 0u);
     };
-    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+    auto store = [&](uint32_t (&r)[32], uint32_t u) {
         const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
-        // inputs < 2q by contract: they feed the GS butterflies directly
-        if constexpr (V == 0 || V == 2) inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
-        if constexpr (V != 1) xpose_p2_to_p1<P>(r, buf, L);
-        if constexpr (V == 0 || V == 2) inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
         if (LT::BIG || poly < npoly) {
             uint32_t *dst = out + (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
 #pragma unroll
             for (int j = 0; j < 32; ++j) {
                 if constexpr (V == 2) asm volatile("" ::"v"(r[j]));
-                else dst[LT::S * j] = r[j];
+                else st_out(dst + LT::S * j, r[j]);
             }
         }
     };
+    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+        // inputs < 2q by contract: they feed the GS butterflies directly
+        if constexpr (V == 0 || V == 2) inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        if constexpr (V != 1) xpose_p2_to_p1<P>(r, buf, L);
+        if constexpr (V == 0 && NTT_INV_EMIT) {
+            const uint32_t poly = u * PPW + (LT::BIG ? 0u : L.h);
+            uint32_t *dst = out + (size_t)poly * P::N + L.brl;
+            const bool valid = LT::BIG || poly < npoly;
+            auto emit = [&](int j, uint32_t v) {
+                if (valid) st_out(dst + LT::S * j, v);
+            };
+            inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
+            return;
+        }
+        if constexpr (V == 0 || V == 2) inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        store(r, u);
+    };
+    if constexpr (NTT_DMA && V == 0) {
+        const uint32_t *nb = buf + (LT::BIG ? 0u : 1024u * L.h) + L.brl;   // natural image, pass-2 (bit-reversed) layout
+        auto read = [&](uint32_t (&r)[32]) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) r[j] = nb[LT::S * brv5(j)];
+        };
+        auto front = [&](uint32_t (&r)[32], uint32_t) {
+            inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+            xpose_p2_to_p1<P>(r, buf, L);
+        };
+        auto back = [&](uint32_t (&r)[32], uint32_t u) {
+            inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+            store(r, u);
+        };
+        chunk_loop_dma<WAVES>(in, npoly, nunits, ppw, lds_addr(buf), L.lane, !LT::BIG, prologue, read, front, back);
+        return;
+    }
     chunk_loop<WAVES>(nunits, ppw, prologue, load, process);
 }
 

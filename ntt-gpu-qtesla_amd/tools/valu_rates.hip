@@ -28,6 +28,38 @@ OP_KERNEL(k_mul_lo, "v_mul_lo_u32 %0, %0, %1")
 OP_KERNEL(k_mul_hi, "v_mul_hi_u32 %0, %0, %1")
 OP_KERNEL(k_mul_u24, "v_mul_u32_u24 %0, %0, %1")
 OP_KERNEL(k_mulhi_u24, "v_mul_hi_u32_u24 %0, %0, %1")
+OP_KERNEL(k_add3, "v_add3_u32 %0, %0, %1, %1")
+OP_KERNEL(k_mad_u24, "v_mad_u32_u24 %0, %0, %1, %1")
+OP_KERNEL(k_fma_f32, "v_fma_f32 %0, %0, %1, %1")
+OP_KERNEL(k_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
+OP_KERNEL(k_perm, "v_perm_b32 %0, %0, %1, %1")
+
+__global__ __launch_bounds__(256) void k_fma64(unsigned *out, unsigned seed, int iters)
+{
+    double a[8];
+    for (int k = 0; k < 8; k++) a[k] = threadIdx.x + k + seed;
+    double b = 1.0000001 * seed;
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(a[k]) : "v"(b));
+    }
+    unsigned r = 0;
+    for (int k = 0; k < 8; k++) r ^= (unsigned)a[k];
+    out[blockIdx.x * 256 + threadIdx.x] = r;
+}
+__global__ __launch_bounds__(256) void k_pk_add(unsigned *out, unsigned seed, int iters)
+{
+    unsigned long long a[8];
+    for (int k = 0; k < 8; k++) a[k] = threadIdx.x + k + seed;
+    unsigned long long b = seed | 1;
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(*(unsigned *)&a[k]) : "v"((unsigned)b));
+    }
+    unsigned r = 0;
+    for (int k = 0; k < 8; k++) r ^= (unsigned)a[k];
+    out[blockIdx.x * 256 + threadIdx.x] = r;
+}
 
 __global__ __launch_bounds__(256) void k_mad64(unsigned *out, unsigned seed, int iters)
 {
@@ -53,7 +85,9 @@ int main()
     hipMalloc(&out, blocks * 256 * 4);
     struct K { const char *name; void (*fn)(unsigned *, unsigned, int); };
     K ks[] = {{"v_add_u32", k_add}, {"v_min_u32", k_min}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_hi_u32", k_mul_hi},
-              {"v_mul_u32_u24", k_mul_u24}, {"v_mul_hi_u32_u24", k_mulhi_u24}, {"v_mad_u64_u32", k_mad64}};
+              {"v_mul_u32_u24", k_mul_u24}, {"v_mul_hi_u32_u24", k_mulhi_u24}, {"v_mad_u64_u32", k_mad64},
+              {"v_add3_u32", k_add3}, {"v_mad_u32_u24", k_mad_u24}, {"v_fma_f32", k_fma_f32},
+              {"v_cndmask_b32", k_cndmask}, {"v_perm_b32", k_perm}, {"v_fma_f64", k_fma64}, {"v_pk_add_u16", k_pk_add}};
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
@@ -67,8 +101,8 @@ int main()
         float ms;
         hipEventElapsedTime(&ms, e0, e1);
         double lane_ops = (double)blocks * 256 * iters * 8;
-        printf(", \"%s\": {\"lane_ops_per_s\": %.4e, \"lanes_per_clk_per_cu_at_2.4GHz\": %.2f}", k.name,
-               lane_ops / (ms * 1e-3), lane_ops / (ms * 1e-3) / 2.4e9 / cus);
+        printf(",\n \"%s\": {\"ms\": %.3f, \"lane_ops_per_s\": %.4e, \"lanes_per_clk_per_cu_at_2.4GHz\": %.2f}", k.name,
+               ms, lane_ops / (ms * 1e-3), lane_ops / (ms * 1e-3) / 2.4e9 / cus);
     }
     printf("}\n");
     hipFree(out);
