@@ -111,7 +111,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--param", default="p-III")
     ap.add_argument("--batch", type=int, default=1 << 20, help="polynomials per GPU")
-    ap.add_argument("--op", default="fwdinv", choices=["fwdinv", "fwd", "inv", "polymul", "nussbaumer"])
+    ap.add_argument("--op", default="fwdinv",
+                    choices=["fwdinv", "fwd", "inv", "polymul", "nussbaumer", "polymul_host", "fwdinv_host"])
+    ap.add_argument("--pageable", action="store_true", help="*_host ops: pageable instead of pinned host buffers")
+    ap.add_argument("--chunk", type=int, default=0, help="*_host ops: polys per chunk (0 = library default)")
+    ap.add_argument("--slots", type=int, default=0, help="*_host ops: buffer slots (0 = library default)")
     ap.add_argument("--ring", default="q", choices=["q", "m32"], help="--op nussbaumer: mod q or mod 2^32-1")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -129,6 +133,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=device)
+
+    if args.op.endswith("_host"):
+        return bench_host(args, ntt_amd, torch, device, rank, world)
 
     pinfo = ntt_amd.param_info(args.param)
     n = pinfo["n"]
@@ -233,6 +240,75 @@ def main():
         dist.destroy_process_group()
     if ok is False:
         sys.exit(1)
+
+
+def bench_host(args, ntt_amd, torch, device, rank, world):
+    """Host -> host operation through ntt_host_ctx: the
+    reference's PCIe-inclusive timing (NTT.cu:2384-2428), pipelined.  Never
+    the headline `value` of the device-resident metric."""
+    import numpy as np
+    pinfo = ntt_amd.param_info(args.param)
+    n = pinfo["n"]
+    B = args.batch
+    first, count = shard(B, rank)
+    nin = 2 if args.op == "polymul_host" else 1
+
+    def host_buf(seed):
+        t = torch.empty(count * n, dtype=torch.int32, device=device)
+        if seed is not None:
+            ntt_amd.fill_uniform(t, args.param, seed, first)
+        arr = np.empty((count, n), np.uint32) if args.pageable else ntt_amd.host_empty(count * n).reshape(count, n)
+        arr[...] = t.cpu().numpy().view(np.uint32).reshape(count, n)
+        return arr
+
+    a = host_buf(SEED)
+    b = host_buf(SEED ^ 0xFFFF) if nin == 2 else None
+    c = host_buf(None)
+    ctx = ntt_amd.HostContext(args.param, args.chunk, args.slots)
+
+    def step():
+        if nin == 2:
+            ctx.mul(c, a, b)
+        else:
+            ctx.ntt(c, a)
+            ctx.invntt(c, c)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world, device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    t1 = time.perf_counter()
+    barrier(world, device)
+    elapsed = max_over_ranks(t1 - t0, world, device)
+    ok = None
+    if not args.no_check:
+        ok = bool(np.array_equal(c, a)) if nin == 1 else None
+    ctx.close()
+    units = world * count * args.steps
+    value = units / elapsed
+    # PCIe bytes per unit: polymul 2 in + 1 out; fwd+inv 2 in + 2 out
+    pcie_bytes = (3 if nin == 2 else 4) * n * 4
+    workload = ("host->host fused negacyclic poly-mul" if nin == 2 else "host->host fwd+inv negacyclic NTT") + \
+        f" n={n} qTESLA-{args.param} ({'pageable' if args.pageable else 'pinned'} buffers, PCIe in the timed region)"
+    out = {
+        "metric": f"{'products/s' if nin == 2 else 'fwd+inv pairs/s'} ({workload})",
+        "value": value, "unit": "products/s" if nin == 2 else "fwd+inv pairs/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic (device counter-based uniform coefficients in [0,q))",
+        "config": {"workload": workload, "param_set": args.param, "n": n, "batch_per_gpu": count,
+                   "chunk_polys": args.chunk or 4096, "slots": args.slots or 3,
+                   "global_batch": world * count, "parallelism": f"batch-shard x{world}"},
+        "pcie_gbs": value * pcie_bytes / 1e9 / world,
+        "check": {"roundtrip_identity_full_batch": ok},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

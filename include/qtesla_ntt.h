@@ -118,6 +118,32 @@ int poly_pointwise(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,
 int ntt_fill_uniform(uint32_t *d_poly, size_t batch, int param_set,
                      uint64_t seed, uint64_t first_poly, void *stream);
 
+/* ---- host-buffer (streamed) operation --------------------------------- */
+/* The reference times its GPU pipelines host -> host: synchronous H2D, the
+ * kernel sequence and D2H on the default stream (NTT.cu:2384-2428; SURVEY.md
+ * §8(f) row 4).  A context pipelines that in chunks of `chunk_polys`
+ * polynomials (0 -> 4096) over three event-chained HIP queues (H2D copies,
+ * kernels, D2H copies) and `nslots` buffer slots (0 -> 3, at most 8):
+ * chunk i's D2H, chunk i+1's kernel and chunk i+2's H2D overlap.  Each slot
+ * owns 3 device and 3 pinned host buffers of chunk_polys*n words, on the
+ * device that is current at creation.  Pinned host buffers (ntt_host_alloc,
+ * hipHostMalloc, registered memory) are DMA'd directly; pageable ones are
+ * staged through the slots' pinned buffers by host memcpy.  The calls are
+ * synchronous: on return the outputs are in host memory.  h_out may equal
+ * an input (in place); other overlaps are undefined.  A context serves one
+ * host thread at a time. */
+typedef struct ntt_host_ctx ntt_host_ctx;
+int ntt_host_ctx_create(ntt_host_ctx **ctx, int param_set, size_t chunk_polys, int nslots);
+int ntt_host_ctx_destroy(ntt_host_ctx *ctx);
+/* host -> host forward / inverse transform (poly_ntt_oop / poly_invntt_oop) */
+int poly_ntt_host(ntt_host_ctx *ctx, uint32_t *h_out, const uint32_t *h_in, size_t batch);
+int poly_invntt_host(ntt_host_ctx *ctx, uint32_t *h_out, const uint32_t *h_in, size_t batch);
+/* host -> host fused negacyclic product (poly_mul) */
+int poly_mul_host(ntt_host_ctx *ctx, uint32_t *h_c, const uint32_t *h_a, const uint32_t *h_b, size_t batch);
+/* pinned host memory for the calls above (NULL on failure) */
+void *ntt_host_alloc(size_t bytes);
+void ntt_host_free(void *p);
+
 /* Last HIP error code seen by this thread (hipError_t as int), and a
  * static string for an NTT_ERR_* code. */
 int ntt_last_hip_error(void);

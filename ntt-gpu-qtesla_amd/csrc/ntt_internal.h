@@ -12,6 +12,8 @@ int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uint32_t *d_in
 }
 namespace qntt {
 /* csrc/nussbaumer.hip: launches the Nussbaumer kernel; returns a hipError_t */
+/* csrc/ntt_kernels.hip: records a hipError_t for ntt_last_hip_error() */
+void set_last_hip(int e);
 int nussbaumer_launch(int ps, int ring, const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch,
                       void *stream, int cus);
 }

@@ -1078,6 +1078,9 @@ int transform(bool inverse, uint32_t *out, const uint32_t *in, size_t batch, int
 }
 
 }  // namespace
+
+void set_last_hip(int e) { t_last_hip = e; }
+
 }  // namespace qntt
 
 // ==========================================================================

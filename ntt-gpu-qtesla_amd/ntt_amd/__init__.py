@@ -61,6 +61,15 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(
                 f"HIP library {LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        # One HIP runtime per process: torch ships its own libamdhip64, loaded
+        # into the global scope when torch is imported.  Importing it first
+        # makes this library's hip* references bind to that same runtime; a
+        # second runtime initialised after torch's finds no device
+        # (hipErrorNoDevice from the host-buffer context, measured).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         L.ntt_param_info.argtypes = [ctypes.c_int] + [_u32p] * 6
         L.ntt_get_tables.argtypes = [ctypes.c_int] + [_u32p] * 5
@@ -76,6 +85,14 @@ def lib():
         L.ntt_strerror.restype = ctypes.c_char_p
         L.ntt_strerror.argtypes = [ctypes.c_int]
         L.ntt_build_info.argtypes = [ctypes.c_char_p, _sz]
+        L.ntt_host_ctx_create.argtypes = [ctypes.POINTER(_vp), ctypes.c_int, _sz, ctypes.c_int]
+        L.ntt_host_ctx_destroy.argtypes = [_vp]
+        for nm in ("poly_ntt_host", "poly_invntt_host"):
+            getattr(L, nm).argtypes = [_vp, _vp, _vp, _sz]
+        L.poly_mul_host.argtypes = [_vp, _vp, _vp, _vp, _sz]
+        L.ntt_host_alloc.argtypes = [_sz]
+        L.ntt_host_alloc.restype = _vp
+        L.ntt_host_free.argtypes = [_vp]
         _lib = L
     return _lib
 
@@ -234,3 +251,86 @@ def to_numpy_u32(t) -> np.ndarray:
 def from_numpy_u32(a: np.ndarray, device="cuda"):
     torch = _torch()
     return torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32)).to(device)
+
+
+# ------------------------------------------------------- host-buffer API
+# Host -> host operation pipelined over HIP streams (include/qtesla_ntt.h,
+# "host-buffer (streamed) operation"; the reference's PCIe-inclusive driver
+# body NTT.cu:2384-2428).  Arrays are numpy uint32, C-contiguous [batch, n].
+
+class HostContext:
+    """Owns the device / pinned staging buffers of ntt_host_ctx_create."""
+
+    def __init__(self, param_set, chunk_polys: int = 0, nslots: int = 0):
+        self.param_set = param_set
+        self.n = param_info(param_set)["n"]
+        h = _vp()
+        _check(lib().ntt_host_ctx_create(ctypes.byref(h), _ps(param_set), chunk_polys, nslots),
+               "ntt_host_ctx_create")
+        self._h = h
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            _check(lib().ntt_host_ctx_destroy(self._h), "ntt_host_ctx_destroy")
+        self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _arr(self, x, name):
+        if not isinstance(x, np.ndarray) or x.dtype != np.uint32 or not x.flags["C_CONTIGUOUS"]:
+            raise TypeError(f"{name}: expected a C-contiguous numpy uint32 array")
+        if x.size % self.n:
+            raise ValueError(f"{name}: size {x.size} is not a multiple of n={self.n}")
+        return x.size // self.n
+
+    def ntt(self, out, inp):
+        b = self._arr(inp, "inp")
+        if self._arr(out, "out") != b:
+            raise ValueError("out/in batch mismatch")
+        _check(lib().poly_ntt_host(self._h, out.ctypes.data, inp.ctypes.data, b), "poly_ntt_host")
+        return out
+
+    def invntt(self, out, inp):
+        b = self._arr(inp, "inp")
+        if self._arr(out, "out") != b:
+            raise ValueError("out/in batch mismatch")
+        _check(lib().poly_invntt_host(self._h, out.ctypes.data, inp.ctypes.data, b), "poly_invntt_host")
+        return out
+
+    def mul(self, c, a, b):
+        nb = self._arr(a, "a")
+        if self._arr(b, "b") != nb or self._arr(c, "c") != nb:
+            raise ValueError("batch mismatch")
+        _check(lib().poly_mul_host(self._h, c.ctypes.data, a.ctypes.data, b.ctypes.data, nb), "poly_mul_host")
+        return c
+
+
+def host_empty(count: int) -> np.ndarray:
+    """A numpy uint32 array of `count` words in pinned host memory (ntt_host_alloc).
+
+    The memory is freed when the last array viewing it is garbage-collected
+    (the ctypes buffer below is the numpy base of every view)."""
+    words = max(int(count), 1)
+    ptr = lib().ntt_host_alloc(words * 4)
+    if not ptr:
+        raise MemoryError("ntt_host_alloc failed")
+
+    def _free(self):
+        if getattr(self, "_ptr", None):
+            lib().ntt_host_free(self._ptr)
+            self._ptr = None
+
+    buf_t = type("PinnedU32", (ctypes.c_uint32 * words,), {"__del__": _free})
+    buf = buf_t.from_address(ptr)
+    buf._ptr = ptr
+    return np.frombuffer(buf, dtype=np.uint32, count=int(count))

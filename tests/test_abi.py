@@ -50,3 +50,14 @@ def test_cpu_tensor_rejected(ntt):
     torch = pytest.importorskip("torch")
     with pytest.raises(ValueError):
         ntt.poly_ntt(torch.zeros(2048, dtype=torch.int32), "p-III")
+
+
+def test_host_ctx_validation_without_gpu(ntt):
+    import ctypes
+    L = ntt.lib()
+    h = ctypes.c_void_p()
+    assert L.ntt_host_ctx_create(None, 0, 0, 0) == ntt.NTT_ERR_NULL
+    assert L.ntt_host_ctx_create(ctypes.byref(h), 5, 0, 0) == ntt.NTT_ERR_PARAM
+    assert L.ntt_host_ctx_create(ctypes.byref(h), 0, 0, 9) == ntt.NTT_ERR_SIZE
+    assert L.ntt_host_ctx_destroy(None) == ntt.NTT_ERR_NULL
+    assert L.poly_mul_host(None, None, None, None, 1) == ntt.NTT_ERR_NULL
