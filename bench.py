@@ -71,17 +71,26 @@ def cpu_baseline(param: str, seconds: float, threads: int = 1) -> dict:
     import oracle as O
     if not os.path.exists(O.LIB_PATH):
         O.build()
+    # scale the sample to ~`seconds` of wall time (two refinements: a tiny
+    # first sample under-estimates the per-poly time of a multi-thread run)
     count = 8 * threads
-    x = O.fill_uniform(count, param, SEED, 0)
-    t = O.time_fwd_inv(x, param, threads, 1)
-    # scale the sample to ~`seconds` of CPU work
-    count = max(count, int(count * seconds / max(t, 1e-6)))
-    count = min(count, 1 << 16)
-    x = O.fill_uniform(count, param, SEED, 0)
-    t = O.time_fwd_inv(x, param, threads, 1)
+    for _ in range(3):
+        x = O.fill_uniform(count, param, SEED, 0)
+        t = O.time_fwd_inv(x, param, threads, 1)
+        if t >= 0.5 * seconds or count >= (1 << 20):
+            break
+        count = min(max(count, int(count * seconds / max(t, 1e-6))), 1 << 20)
     n = O.params(param)["n"]
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {
         "value": count / t,
+        "cpu_model": cpu,
+        "nproc": os.cpu_count(),
         "unit": "fwd+inv pairs/s",
         "cores": threads,
         "kind": "port",
@@ -233,6 +242,9 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.param, args.cpu_seconds, 1)
+        # the same restatement batch-parallel over this box's CPU share
+        threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+        out["cpu_baseline_all_cores"] = cpu_baseline(args.param, args.cpu_seconds / 2, threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
