@@ -494,6 +494,10 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
 // its completion is counted by hand.  vmcnt counts loads, stores and LDS-DMA
 // together in issue order (MI355X_MICROARCH.md), and exactly 32 stores follow
 // each DMA, so `s_waitcnt vmcnt(32)` retires precisely the DMA.
+// Bit-exact but measured neutral on p-III (fwd +-0 %, inv +1.7 %, interleaved
+// A/B, profiles/r01/ab_ntstore_dma.json): the memory side of this access shape
+// is not latency-bound at 4 waves/SIMD (tools/copy_bw.hip "occ" modes), so the
+// option stays off.
 // ------------------------------------------------------------------------
 #ifndef NTT_DMA
 #define NTT_DMA 0
