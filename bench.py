@@ -121,7 +121,8 @@ def main():
     ap.add_argument("--param", default="p-III")
     ap.add_argument("--batch", type=int, default=1 << 20, help="polynomials per GPU")
     ap.add_argument("--op", default="fwdinv",
-                    choices=["fwdinv", "fwd", "inv", "polymul", "nussbaumer", "polymul_host", "fwdinv_host"])
+                    choices=["fwdinv", "fwd", "inv", "polymul", "polymul_ntt", "nussbaumer", "polymul_host",
+                             "fwdinv_host"])
     ap.add_argument("--pageable", action="store_true", help="*_host ops: pageable instead of pinned host buffers")
     ap.add_argument("--chunk", type=int, default=0, help="*_host ops: polys per chunk (0 = library default)")
     ap.add_argument("--slots", type=int, default=0, help="*_host ops: buffer slots (0 = library default)")
@@ -153,7 +154,7 @@ def main():
     x = torch.empty(count * n, dtype=torch.int32, device=device)
     ntt_amd.fill_uniform(x, args.param, SEED, first)
     y = z = None
-    if args.op in ("polymul", "nussbaumer"):
+    if args.op in ("polymul", "polymul_ntt", "nussbaumer"):
         y = torch.empty_like(x)
         z = torch.empty_like(x)
         ntt_amd.fill_uniform(y, args.param, SEED ^ 0xFFFF, first)
@@ -166,10 +167,12 @@ def main():
             ntt_amd.poly_invntt(x, args.param, stream)
         elif kind == "mul":
             ntt_amd.poly_mul(z, x, y, args.param, stream)
+        elif kind == "mulntt":
+            ntt_amd.poly_mul_ntt(z, x, y, args.param, stream)
         else:
             ntt_amd.poly_mul_nussbaumer(z, x, y, args.param, args.ring, stream)
 
-    kinds = {"fwdinv": ["fwd", "inv"], "fwd": ["fwd"], "inv": ["inv"], "polymul": ["mul"],
+    kinds = {"fwdinv": ["fwd", "inv"], "fwd": ["fwd"], "inv": ["inv"], "polymul": ["mul"], "polymul_ntt": ["mulntt"],
              "nussbaumer": ["nus"]}[args.op]
 
     for _ in range(args.warmup):
@@ -195,7 +198,7 @@ def main():
     per_kind = {k: sum(evs[s][i][0].elapsed_time(evs[s][i][1]) for s in range(args.steps)) / args.steps
                 for i, k in enumerate(kinds)}  # ms per launch
     dom = max(per_kind, key=per_kind.get)
-    bytes_per_coeff = 12 if dom in ("mul", "nus") else 8
+    bytes_per_coeff = 12 if dom in ("mul", "mulntt", "nus") else 8
     alg_bytes = count * n * bytes_per_coeff
     achieved = alg_bytes / (per_kind[dom] * 1e-3) / 1e9
 
@@ -213,9 +216,11 @@ def main():
     value = units / elapsed
     workload = {"fwdinv": "fwd+inv negacyclic NTT", "fwd": "forward negacyclic NTT",
                 "inv": "inverse negacyclic NTT", "polymul": "fused negacyclic poly-mul",
+                "polymul_ntt": "fused negacyclic poly-mul, second operand in the NTT domain",
                 "nussbaumer": "Nussbaumer negacyclic product" + (" mod 2^32-1" if args.ring == "m32" else "")}[args.op]
     workload = f"{workload} n={n} qTESLA-{args.param}" if args.param != "ref" else f"{workload} n={n} ref q={pinfo['q']}"
     unit = {"fwdinv": "fwd+inv pairs/s", "fwd": "NTTs/s", "inv": "INTTs/s", "polymul": "products/s",
+            "polymul_ntt": "products/s",
             "nussbaumer": "products/s"}[args.op]
     out = {
         "metric": METRIC if args.op == "fwdinv" and args.param == "p-III" else f"{unit} ({workload})",

@@ -91,6 +91,16 @@ int poly_invntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch,
 int poly_mul(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,
              size_t batch, int param_set, void *stream);
 
+/* Fused product with the second operand already in the NTT domain:
+ *   c = a * b mod (x^n + 1, q)  where  d_bhat = poly_ntt(b)  (natural order,
+ *   this library's psi, entries < 2q).
+ * qTESLA samples its public polynomial directly in the NTT domain; this is
+ * the CT-GS driver (NTT.cu:2388-2425) with the second forward transform
+ * (:2402-2411) dropped: two transforms of work per product instead of three.
+ * d_c may alias d_a or d_bhat. */
+int poly_mul_ntt(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_bhat,
+                 size_t batch, int param_set, void *stream);
+
 /* Nussbaumer negacyclic product (the paper's alternate algorithm): the
  * reference's single-polynomial CPU routine nussbaumer_fft (NTT.cu:167-277,
  * driver test_nussbaumer :1987-2005), batched on the GPU and extended from

@@ -439,8 +439,15 @@ __device__ __forceinline__ constexpr uint32_t brv5(int j)
 #ifndef NTT_WG
 #define NTT_WG 512          // fwd / inv: 8 waves, 64 + 15.5 KiB LDS -> 2 WG/CU
 #endif
+// poly_mul workgroup per parameter set: n=2048 runs 16 waves (128 + 31.5 KiB
+// LDS, 1 WG/CU, <=128 VGPRs -> 4 waves/SIMD, 6 spilled VGPRs: -1..-2 % time);
+// n=1024 keeps 8 waves at <=256 VGPRs (2 waves/SIMD; at 128 VGPRs it spills 60
+// and loses 37 %), profiles/r01/ab_poly_mul_wg.json
 #ifndef MUL_WG
-#define MUL_WG 512          // poly_mul: 8 waves, 64 + 31.5 KiB LDS -> 1 WG/CU (2 waves/SIMD beat 3-4: spills)
+#define MUL_WG 512
+#endif
+#ifndef MUL_WG_BIG
+#define MUL_WG_BIG 1024
 #endif
 #ifndef NTT_WAVES_PER_SIMD
 #define NTT_WAVES_PER_SIMD 4
@@ -448,6 +455,11 @@ __device__ __forceinline__ constexpr uint32_t brv5(int j)
 #ifndef MUL_WAVES_PER_SIMD
 #define MUL_WAVES_PER_SIMD 2
 #endif
+#ifndef MUL_WAVES_PER_SIMD_BIG
+#define MUL_WAVES_PER_SIMD_BIG 4
+#endif
+template <int PS> constexpr int mul_wg() { return PSel<PS>::T::LOGN == 11 ? MUL_WG_BIG : MUL_WG; }
+template <int PS> constexpr int mul_occ() { return PSel<PS>::T::LOGN == 11 ? MUL_WAVES_PER_SIMD_BIG : MUL_WAVES_PER_SIMD; }
 constexpr int WG = 256;             // elementwise kernels
 
 // Work distribution: workgroup b owns the contiguous unit range
@@ -751,19 +763,22 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
 
 // fused c = a*b mod (x^n+1): FWD(a), FWD(b), Montgomery pointwise (the 2^-32
 // is folded into the inverse's final n^-1 scaling), INV -- one HBM read of a
-// and b, one write of c.
-template <int PS>
-__global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
+// and b, one write of c.  BHAT: b is given already transformed (natural-order
+// output of poly_ntt), so only a is transformed -- two transforms of work per
+// product instead of three (poly_mul_ntt).
+template <int PS, bool BHAT = false>
+__global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
 {
     using P = typename PSel<PS>::T;
     using LT = Lane<P>;
     constexpr uint32_t PPW = LT::BIG ? 1 : 2;
-    constexpr int WAVES = MUL_WG / 64;
+    constexpr int WG_ = mul_wg<PS>();
+    constexpr int WAVES = WG_ / 64;
     __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + 2 * TW2_WORDS];
     uint2 *ftw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
     uint2 *itw2 = ftw2 + TW2_WORDS / 2;
-    fill_tw2<PS, false, MUL_WG>(ftw2);
-    fill_tw2<PS, true, MUL_WG>(itw2);
+    fill_tw2<PS, false, WG_>(ftw2);
+    fill_tw2<PS, true, WG_>(itw2);
     __syncthreads();
     const LT L;
     uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
@@ -788,20 +803,24 @@ __global__ __launch_bounds__(MUL_WG, MUL_WAVES_PER_SIMD) void k_poly_mul(const u
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
             ra[j] = umin(ra[j], ra[j] - P::Q2);
-            rb[j] = valid ? pb[LT::S * j] : 0u;
+            // b-hat is in natural order: register j of the pass-2 layout holds
+            // index brv5(j)*S + lane (the forward's store mapping)
+            rb[j] = valid ? pb[LT::S * (BHAT ? brv5(j) : (uint32_t)j)] : 0u;
         }
-        fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
-        xpose_p1_to_p2<P>(rb, buf, L);
-        fwd_pass2<P>(rb, ftw2 + opaque_zero(), L.lane);
+        if constexpr (!BHAT) {
+            fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+            xpose_p1_to_p2<P>(rb, buf, L);
+            fwd_pass2<P>(rb, ftw2 + opaque_zero(), L.lane);
+        }
 #pragma unroll
-        for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(ra[j], umin(rb[j], rb[j] - P::Q2));
+        for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(ra[j], umin(rb[j], rb[j] - P::Q2));   // b-hat < 2q
         inv_pass2<P>(ra, itw2 + opaque_zero(), L.lane);
         xpose_p2_to_p1<P>(ra, buf, L);
-        inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero());
-        if (valid) {
-#pragma unroll
-            for (int j = 0; j < 32; ++j) c[off + LT::S * j] = ra[j];
-        }
+        uint32_t *pc = c + off;
+        auto emit = [&](int j, uint32_t v) {   // stores interleaved with the last stage (see k_ntt_inv)
+            if (valid) st_out(pc + LT::S * j, v);
+        };
+        inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
     }
 }
 
@@ -977,9 +996,9 @@ const DevInfo &dev_info()
         d.occ[1][0] = blocks_per_cu(k_ntt_inv<0>, NTT_WG);
         d.occ[1][1] = blocks_per_cu(k_ntt_inv<1>, NTT_WG);
         d.occ[1][2] = blocks_per_cu(k_ntt_inv<2>, NTT_WG);
-        d.occ[2][0] = blocks_per_cu(k_poly_mul<0>, MUL_WG);
-        d.occ[2][1] = blocks_per_cu(k_poly_mul<1>, MUL_WG);
-        d.occ[2][2] = blocks_per_cu(k_poly_mul<2>, MUL_WG);
+        d.occ[2][0] = blocks_per_cu(k_poly_mul<0, false>, mul_wg<0>());
+        d.occ[2][1] = blocks_per_cu(k_poly_mul<1, false>, mul_wg<1>());
+        d.occ[2][2] = blocks_per_cu(k_poly_mul<2, false>, mul_wg<2>());
     });
     return g_dev[dev];
 }
@@ -992,7 +1011,7 @@ Launch launch_for(int op, int ps, size_t npoly)
 {
     const size_t upw = param_set(ps)->logn == 11 ? 1 : 2;
     const size_t units = (npoly + upw - 1) / upw;
-    const size_t waves = (size_t)(op == 2 ? MUL_WG : NTT_WG) / 64;
+    const size_t waves = (size_t)(op == 2 ? (param_set(ps)->logn == 11 ? MUL_WG_BIG : MUL_WG) : NTT_WG) / 64;
     const size_t min_groups = (size_t)dev_info().cus * 4;
     size_t ppw = units / (waves * min_groups);
     ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
@@ -1051,10 +1070,11 @@ template <int PS> struct LInv {
     }
 };
 template <int PS> struct LMul {
-    static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s)
+    static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s, bool bhat)
     {
         const Launch l = launch_for(2, PS, batch);
-        hipLaunchKernelGGL(k_poly_mul<PS>, dim3(l.grid), dim3(MUL_WG), 0, s, a, b, c, (uint32_t)batch, l.ppw);
+        if (bhat) hipLaunchKernelGGL((k_poly_mul<PS, true>), dim3(l.grid), dim3(mul_wg<PS>()), 0, s, a, b, c, (uint32_t)batch, l.ppw);
+        else hipLaunchKernelGGL((k_poly_mul<PS, false>), dim3(l.grid), dim3(mul_wg<PS>()), 0, s, a, b, c, (uint32_t)batch, l.ppw);
         return finish_launch();
     }
 };
@@ -1145,7 +1165,8 @@ int poly_invntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch, int ps,
     return transform(true, d_out, d_in, batch, ps, stream);
 }
 
-int poly_mul(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t batch, int ps, void *stream)
+static int mul_common(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t batch, int ps, void *stream,
+                      bool bhat)
 {
     int rc;
     if ((rc = check_common(ps, d_a, batch)) != NTT_OK || batch == 0) return rc;
@@ -1154,7 +1175,17 @@ int poly_mul(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t bat
     const size_t bytes = batch * param_set(ps)->n * 4;
     if (partial_overlap(d_a, d_c, bytes) || partial_overlap(d_b, d_c, bytes)) return NTT_ERR_ALIAS;
     if ((rc = ensure_device_tables()) != NTT_OK) return rc;
-    return dispatch<LMul>(ps, d_a, d_b, d_c, batch, (hipStream_t)stream);
+    return dispatch<LMul>(ps, d_a, d_b, d_c, batch, (hipStream_t)stream, bhat);
+}
+
+int poly_mul(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t batch, int ps, void *stream)
+{
+    return mul_common(d_c, d_a, d_b, batch, ps, stream, false);
+}
+
+int poly_mul_ntt(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_bhat, size_t batch, int ps, void *stream)
+{
+    return mul_common(d_c, d_a, d_bhat, batch, ps, stream, true);
 }
 
 int poly_mul_nussbaumer(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t batch, int ps, int ring,

@@ -77,7 +77,7 @@ def lib():
             getattr(L, nm).argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
         for nm in ("poly_ntt_oop", "poly_invntt_oop"):
             getattr(L, nm).argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
-        for nm in ("poly_mul", "poly_pointwise"):
+        for nm in ("poly_mul", "poly_mul_ntt", "poly_pointwise"):
             getattr(L, nm).argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, _vp]
         L.poly_mul_nussbaumer.argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp]
         L.ntt_fill_uniform.argtypes = [_vp, _sz, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp]
@@ -208,6 +208,17 @@ def poly_mul(c, a, b, param_set, stream=None):
     if _batch(b, n) != nb or _batch(c, n) != nb:
         raise ValueError("batch mismatch")
     _check(lib().poly_mul(c.data_ptr(), a.data_ptr(), b.data_ptr(), nb, _ps(param_set), _stream(stream)), "poly_mul")
+    return c
+
+
+def poly_mul_ntt(c, a, bhat, param_set, stream=None):
+    """c = a*b mod (x^n + 1, q) with bhat = poly_ntt(b) given (NTT domain)."""
+    n = param_info(param_set)["n"]
+    nb = _batch(a, n)
+    if _batch(bhat, n) != nb or _batch(c, n) != nb:
+        raise ValueError("batch mismatch")
+    _check(lib().poly_mul_ntt(c.data_ptr(), a.data_ptr(), bhat.data_ptr(), nb, _ps(param_set), _stream(stream)),
+           "poly_mul_ntt")
     return c
 
 

@@ -195,8 +195,18 @@ def test_full_batch_properties(ntt, oracle, dev, ps, batch):
     assert np.array_equal(ntt.to_numpy_u32(X), oracle.poly_ntt(xs, ps))
     ntt.poly_invntt(x, ps)
     assert torch.equal(x, ref)
-    # linearity on device: NTT(a) + NTT(b) == NTT(a + b) (mod q), checked on samples
+    # linearity on the whole batch, on device: NTT(a) + NTT(b) == NTT(a + b mod q)
+    q = ntt.param_info(ps)["q"]
+    b = torch.empty_like(x)
+    ntt.fill_uniform(b, ps, 0x5EED0004, 0)
+    s = ((ref.to(torch.int64) & 0xFFFFFFFF) + (b.to(torch.int64) & 0xFFFFFFFF)) % q
+    s = s.to(torch.int32)
     del ref
+    ntt.poly_ntt(x, ps)
+    ntt.poly_ntt(b, ps)
+    ntt.poly_ntt(s, ps)
+    lhs = ((x.to(torch.int64) & 0xFFFFFFFF) + (b.to(torch.int64) & 0xFFFFFFFF)) % q
+    assert torch.equal(lhs, s.to(torch.int64) & 0xFFFFFFFF)
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
@@ -214,3 +224,23 @@ def test_host_driver_kat(ps):
     r = subprocess.run([exe, "-speedgpu", "9", "-param", ps, "-batch", "1000", "-r", "5"], capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0 and "Identical." in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+@pytest.mark.parametrize("batch", [1, 3, 64])
+def test_poly_mul_ntt_domain(ntt, oracle, dev, ps, batch):
+    """poly_mul_ntt(c, a, poly_ntt(b)) == a*b mod (x^n+1, q): the CT-GS driver
+    with b's forward transform done beforehand (qTESLA's NTT-domain operand)."""
+    a = oracle.fill_uniform(batch, ps, 41 + batch, 0)
+    b = oracle.fill_uniform(batch, ps, 42 + batch, 0)
+    want = oracle.poly_mul(a, b, ps)
+    ta = _dev(ntt, a, dev)
+    tb = _dev(ntt, oracle.poly_ntt(b, ps), dev)
+    tc = torch.empty_like(ta)
+    ntt.poly_mul_ntt(tc, ta, tb, ps)
+    assert np.array_equal(_u32(ntt, tc), want)
+    # b-hat entries in [q, 2q) are tolerated; aliasing c with a is allowed
+    q = ntt.param_info(ps)["q"]
+    bl = (oracle.poly_ntt(b, ps).astype(np.uint64) + q).astype(np.uint32)
+    ntt.poly_mul_ntt(ta, ta, _dev(ntt, bl, dev), ps)
+    assert np.array_equal(_u32(ntt, ta), want)

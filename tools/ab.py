@@ -40,6 +40,7 @@ def main():
         for nm in ("poly_ntt_oop", "poly_invntt_oop"):
             getattr(L, nm).argtypes = [vp, vp, sz, ctypes.c_int, vp]
         L.poly_mul.argtypes = [vp, vp, vp, sz, ctypes.c_int, vp]
+        L.poly_mul_ntt.argtypes = [vp, vp, vp, sz, ctypes.c_int, vp]
         libs[os.path.basename(path)] = L
     x = torch.empty(args.batch * n, dtype=torch.int32, device="cuda")
     y = torch.empty_like(x)
@@ -55,6 +56,8 @@ def main():
             rc = L.poly_ntt_oop(dst.data_ptr(), x.data_ptr(), args.batch, ps, s.cuda_stream)
         elif op == "inv":
             rc = L.poly_invntt_oop(dst.data_ptr(), x.data_ptr(), args.batch, ps, s.cuda_stream)
+        elif op == "mulntt":
+            rc = L.poly_mul_ntt(z.data_ptr(), x.data_ptr(), y.data_ptr(), args.batch, ps, s.cuda_stream)
         else:
             rc = L.poly_mul(z.data_ptr(), x.data_ptr(), y.data_ptr(), args.batch, ps, s.cuda_stream)
         assert rc == 0, rc
@@ -65,7 +68,7 @@ def main():
         for op in ops:
             launch(L, op)
             torch.cuda.synchronize()
-            sig = (x if args.inplace and op != "mul" else z)[:: 4099].clone()
+            sig = (x if args.inplace and op in ("fwd", "inv") else z)[:: 4099].clone()
             if op not in ref:
                 ref[op] = sig
             ok[f"{name}:{op}"] = bool(torch.equal(ref[op], sig))
