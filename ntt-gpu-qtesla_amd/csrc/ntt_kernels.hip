@@ -592,6 +592,18 @@ __device__ __forceinline__ void chunk_loop_dma(const uint32_t *in, uint32_t npol
     }
 }
 
+// NTT_PRIO=1: one s_setprio 1 for the second-dispatched half of each
+// workgroup (waves 4-7), the static form of MI355X_MICROARCH.md "Two waves
+// per SIMD" item 4.  Measured: fwd -0.6 %, inv +2.2 % (profiles/r01/ab_prio.json), off.
+#ifndef NTT_PRIO
+#define NTT_PRIO 0
+#endif
+__device__ __forceinline__ void younger_half_priority(int wg)
+{
+    if constexpr (NTT_PRIO)
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= (unsigned)(wg / 2)) __builtin_amdgcn_s_setprio(1);
+}
+
 // V (diagnostic variants, reached only through ntt_debug_variant): 0 = full,
 // 1 = global load + store only, 2 = compute only (no global memory),
 // 3 = load + LDS transpose + store (no arithmetic)
@@ -608,6 +620,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     constexpr int WAVES = NTT_WG / 64;
     __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + TW2_WORDS];
     uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
+    younger_half_priority(NTT_WG);
     auto prologue = [&]() {
         fill_tw2<PS, false, NTT_WG>(tw2);
         __syncthreads();
@@ -697,6 +710,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
     constexpr int WAVES = NTT_WG / 64;
     __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + TW2_WORDS];
     uint2 *tw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
+    younger_half_priority(NTT_WG);
     auto prologue = [&]() {
         fill_tw2<PS, true, NTT_WG>(tw2);
         __syncthreads();
@@ -1006,13 +1020,16 @@ const DevInfo &dev_info()
 // Launch shape: one workgroup per `ppw * waves` consecutive work units.  ppw
 // grows with the batch (amortising the 16 KiB LDS-table prologue) but never
 // beyond what keeps >= 4 workgroups per CU in flight.
+#ifndef NTT_MIN_WG_PER_CU
+#define NTT_MIN_WG_PER_CU 2   // 4 and 8 measured 2-5 % slower on a 65 536-poly n=1024 launch, equal at 2^20 (profiles/r01/ab_launch_shape.json)
+#endif
 struct Launch { uint32_t grid, ppw; };
 Launch launch_for(int op, int ps, size_t npoly)
 {
     const size_t upw = param_set(ps)->logn == 11 ? 1 : 2;
     const size_t units = (npoly + upw - 1) / upw;
     const size_t waves = (size_t)(op == 2 ? (param_set(ps)->logn == 11 ? MUL_WG_BIG : MUL_WG) : NTT_WG) / 64;
-    const size_t min_groups = (size_t)dev_info().cus * 4;
+    const size_t min_groups = (size_t)dev_info().cus * NTT_MIN_WG_PER_CU;
     size_t ppw = units / (waves * min_groups);
     ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
     return {(uint32_t)((units + waves * ppw - 1) / (waves * ppw)), (uint32_t)ppw};
