@@ -84,6 +84,13 @@ int poly_ntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch,
 int poly_invntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch,
                     int param_set, void *stream);
 
+/* Bit-reversal permutation, out[b*n + t] = in[b*n + brv(t)] (log2 n bits),
+ * any 32-bit words.  Replaces bit_reverse_copy_tbl_gpu (NTT.cu:487-492), used
+ * by the CT-CT pipeline (:2239) to feed radix2INTT with bit-reversed input.
+ * d_out may equal d_in (in place); partial overlap is rejected. */
+int poly_bitrev_copy(uint32_t *d_out, const uint32_t *d_in, size_t batch,
+                     int param_set, void *stream);
+
 /* Fused negacyclic product c = a * b mod (x^n + 1, q), natural order.
  * Replaces the whole CT-GS pipeline of test_NTT_CT_GS_nega_gpu
  * (NTT.cu:2388-2425, 34 launches) and CT-CT (NTT.cu:2213-2249) with one

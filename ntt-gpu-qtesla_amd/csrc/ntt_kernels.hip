@@ -639,7 +639,8 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
         for (int j = 0; j < 32; ++j) r[j] = (V == 2 || V == 5) ? L.lane * (j + u) : (valid ? src[LT::S * j] : 0u);
     };
     // V 4/5: V 0/2 with per-phase s_memtime stamps accumulated per wave
-    constexpr bool STAMPS = V >= 4;
+    // V 6: no arithmetic, raw words -- the bit-reversal copy (poly_bitrev_copy)
+    constexpr bool STAMPS = V == 4 || V == 5;
     constexpr bool ALU = V == 0 || V == 2 || V == 4 || V == 5;
     unsigned long long acc[6] = {0, 0, 0, 0, 0, 0}, ts[7];
     // canonical output, bit-reversed registers -> natural order: brv5(j)*S + lane
@@ -650,8 +651,10 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
 #pragma unroll
             for (int j = 0; j < 32; ++j) {
                 uint32_t x = r[j];
-                x = umin(x, x - P::Q2);
-                x = umin(x, x - P::Q);
+                if constexpr (V != 6) {
+                    x = umin(x, x - P::Q2);
+                    x = umin(x, x - P::Q);
+                }
                 if constexpr (V == 2 || V == 5) asm volatile("" ::"v"(x));
                 else st_out(dst + brv5(j) * LT::S, x);
             }
@@ -660,6 +663,14 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     auto process = [&](uint32_t (&r)[32], uint32_t u) {
         if constexpr (STAMPS) NTT_STAMP(ts[0]);
         if constexpr (ALU) fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        if constexpr (V == 6 && LT::BIG) {   // the pass-1 lane-half exchange alone (p1_addr expects it)
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
+                r[2 * m] = pr[0];
+                r[2 * m + 1] = pr[1];
+            }
+        }
         if constexpr (STAMPS) NTT_STAMP(ts[1]);
         if constexpr (V != 1) xpose_p1_to_p2<P>(r, buf, L);
         if constexpr (STAMPS) NTT_STAMP(ts[2]);
@@ -1078,6 +1089,18 @@ template <int PS> struct LFwd {
         return finish_launch();
     }
 };
+// out[t] = in[brv(t)] per polynomial: the forward kernel's load -> LDS
+// transpose -> store path with no arithmetic (V = 6).  Natural-order load,
+// pass-2 register j of lane l holds pos 32*brv6(l) + j, stored at
+// brv(pos) = brv5(j)*S + l: both sides lane-contiguous 256-B runs.
+template <int PS> struct LBitrev {
+    static int run(const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s)
+    {
+        const Launch l = launch_for(0, PS, batch);
+        hipLaunchKernelGGL((k_ntt_fwd<PS, 6>), dim3(l.grid), dim3(NTT_WG), 0, s, in, out, (uint32_t)batch, l.ppw);
+        return finish_launch();
+    }
+};
 template <int PS> struct LInv {
     static int run(const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s)
     {
@@ -1170,6 +1193,16 @@ int poly_invntt(uint32_t *d_poly, const uint32_t *twiddleFactor, size_t batch, i
 {
     (void)twiddleFactor;
     return transform(true, d_poly, d_poly, batch, ps, stream);
+}
+
+int poly_bitrev_copy(uint32_t *d_out, const uint32_t *d_in, size_t batch, int ps, void *stream)
+{
+    int rc = check_common(ps, d_in, batch);
+    if (rc == NTT_OK && batch) rc = check_common(ps, d_out, batch);
+    if (rc != NTT_OK || batch == 0) return rc;
+    if (partial_overlap(d_in, d_out, batch * param_set(ps)->n * 4)) return NTT_ERR_ALIAS;
+    if ((rc = ensure_device_tables()) != NTT_OK) return rc;
+    return dispatch<LBitrev>(ps, d_in, d_out, batch, (hipStream_t)stream);
 }
 
 int poly_ntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch, int ps, void *stream)

@@ -10,6 +10,11 @@
 //   -speedgpu 7   fused poly_mul (one launch per batch)
 //   -speedgpu 8   speed suite: 5 x option 6 then 5 x option 7 (main.cu:213-225)
 //   -speedgpu 9   forward+inverse transform throughput (BASELINE metric)
+//   -speedgpu 10  fused poly-mul host -> host through the pipelined host-buffer
+//                 context (ntt_host_ctx: H2D / kernel / D2H overlapped), the
+//                 reference's PCIe-inclusive timing region (NTT.cu:2384-2428)
+//   -speedgpu 11  Nussbaumer product on the GPU in the reference's ring
+//                 Z/(2^32-1) (test_nussbaumer, NTT.cu:1987-2005; -speedcpu 6 there)
 //   -param ref|p-I|p-III   parameter set (reference: compile-time QTESLA set)
 //   -batch B      polynomials per batch (reference: BATCH macro, main.cuh:7)
 //   -r seed       random operands from the device generator (reference parses
@@ -50,7 +55,7 @@
 
 static void help_message()
 {
-    printf("usage: ntt_main -speedgpu {4,6,7,8,9} [-param ref|p-I|p-III] [-batch B] [-r seed] [-pcie] [-debug]\n");
+    printf("usage: ntt_main -speedgpu {4,6,7,8,9,10,11} [-param ref|p-I|p-III] [-batch B] [-reps R] [-r seed] [-pcie] [-debug]\n");
 }
 
 struct Opts {
@@ -169,6 +174,77 @@ static double run_fwdinv(const Opts &o, int *roundtrip_ok)
     return ms / o.reps;
 }
 
+// host -> host fused product through ntt_host_ctx; all-ones (KAT) or random operands
+static double run_polymul_host(const Opts &o, int *kat_ok)
+{
+    uint32_t n, q;
+    NTT_CALL(ntt_param_info(o.ps, &n, &q, nullptr, nullptr, nullptr, nullptr));
+    const size_t count = o.batch * n, bytes = count * 4;
+    uint32_t *x = (uint32_t *)ntt_host_alloc(bytes), *y = (uint32_t *)ntt_host_alloc(bytes),
+             *z = (uint32_t *)ntt_host_alloc(bytes);
+    if (!x || !y || !z) { fprintf(stderr, "ntt_host_alloc failed\n"); exit(2); }
+    for (size_t i = 0; i < count; i++) x[i] = y[i] = 1;
+    if (o.random) {
+        uint32_t *d;
+        HIP_OK(hipMalloc(&d, bytes));
+        NTT_CALL(ntt_fill_uniform(d, o.batch, o.ps, o.seed, 0, nullptr));
+        HIP_OK(hipMemcpy(x, d, bytes, hipMemcpyDeviceToHost));
+        NTT_CALL(ntt_fill_uniform(d, o.batch, o.ps, o.seed ^ 0xFFFF, 0, nullptr));
+        HIP_OK(hipMemcpy(y, d, bytes, hipMemcpyDeviceToHost));
+        HIP_OK(hipFree(d));
+    }
+    ntt_host_ctx *ctx = nullptr;
+    NTT_CALL(ntt_host_ctx_create(&ctx, o.ps, 0, 0));
+    NTT_CALL(poly_mul_host(ctx, z, x, y, o.batch));   // warm-up
+    double ms = 0.0;
+    for (int r = 0; r < o.reps; r++) {
+        auto t0 = std::chrono::steady_clock::now();
+        NTT_CALL(poly_mul_host(ctx, z, x, y, o.batch));
+        auto t1 = std::chrono::steady_clock::now();
+        ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    }
+    *kat_ok = -1;
+    if (!o.random) {
+        *kat_ok = 1;
+        for (size_t b = 0; b < o.batch && *kat_ok; b++)
+            for (uint32_t k = 0; k < n; k++)
+                if (z[b * n + k] != (uint32_t)((2ull * k + 2 + q - n) % q)) { *kat_ok = 0; break; }
+    }
+    NTT_CALL(ntt_host_ctx_destroy(ctx));
+    ntt_host_free(x);
+    ntt_host_free(y);
+    ntt_host_free(z);
+    return ms / o.reps;
+}
+
+// Nussbaumer mod 2^32-1 on the GPU, all-ones operands: z[k] = 2k + 2 - n mod 2^32-1
+static double run_nussbaumer(const Opts &o, int *kat_ok)
+{
+    uint32_t n;
+    NTT_CALL(ntt_param_info(o.ps, &n, nullptr, nullptr, nullptr, nullptr, nullptr));
+    const size_t count = o.batch * n, bytes = count * 4;
+    std::vector<uint32_t> x(count, 1), z(count, 0);
+    uint32_t *d_x, *d_z;
+    HIP_OK(hipMalloc(&d_x, bytes));
+    HIP_OK(hipMalloc(&d_z, bytes));
+    HIP_OK(hipMemcpy(d_x, x.data(), bytes, hipMemcpyHostToDevice));
+    NTT_CALL(poly_mul_nussbaumer(d_z, d_x, d_x, o.batch, o.ps, NTT_RING_M32, nullptr));
+    HIP_OK(hipDeviceSynchronize());
+    auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < o.reps; r++) NTT_CALL(poly_mul_nussbaumer(d_z, d_x, d_x, o.batch, o.ps, NTT_RING_M32, nullptr));
+    HIP_OK(hipDeviceSynchronize());
+    auto t1 = std::chrono::steady_clock::now();
+    HIP_OK(hipMemcpy(z.data(), d_z, bytes, hipMemcpyDeviceToHost));
+    *kat_ok = 1;
+    const uint64_t m = 0xFFFFFFFFull;
+    for (size_t b = 0; b < o.batch && *kat_ok; b++)
+        for (uint32_t k = 0; k < n; k++)
+            if (z[b * n + k] != (uint32_t)((2ull * k + 2 + m - n) % m)) { *kat_ok = 0; break; }
+    HIP_OK(hipFree(d_x));
+    HIP_OK(hipFree(d_z));
+    return std::chrono::duration<double, std::milli>(t1 - t0).count() / o.reps;
+}
+
 static void report_polymul(const Opts &o, const char *name, bool fused)
 {
     std::vector<uint32_t> z;
@@ -235,6 +311,26 @@ int main(int argc, char **argv)
         printf("fwd+inv n=%u: %.4f ms per batch of %zu -> %.3e pairs/s, %.1f GB/s algorithmic; round trip %s\n", n, ms,
                o.batch, o.batch / ms * 1e3, o.batch * 16.0 * n / ms / 1e6, ok ? "Identical." : "Incorrect result.");
         return ok ? 0 : 1;
+    }
+    case 10: {
+        int kat = -1;
+        const double ms = run_polymul_host(o, &kat);
+        printf("\n========================\ntest_NTT_negacyclic fused host->host (pipelined PCIe). Batch Size is %zu"
+               "\n========================\n", o.batch);
+        printf("Performance GPU fused host->host \n Time\t\t: % .4f ms. \nThroughput\t: %.2f Multiplications per second\n",
+               ms, (double)o.batch / ms * 1000.0);
+        if (kat >= 0) printf("all-ones KAT z[k] = 2k+2-n mod q: %s\n", kat ? "Identical." : "Incorrect result.");
+        return kat == 0 ? 1 : 0;
+    }
+    case 11: {
+        int kat = 0;
+        const double ms = run_nussbaumer(o, &kat);
+        printf("\n========================\ntest_nussbaumer GPU (mod 2^32-1). Batch Size is %zu\n========================\n",
+               o.batch);
+        printf("Performance GPU Nussbaumer \n Time\t\t: % .4f ms. \nThroughput\t: %.2f Multiplications per second\n", ms,
+               (double)o.batch / ms * 1000.0);
+        printf("all-ones KAT z[k] = 2k+2-n mod 2^32-1: %s\n", kat ? "Identical." : "Incorrect result.");
+        return kat ? 0 : 1;
     }
     default: help_message(); return -1;
     }

@@ -75,7 +75,7 @@ def lib():
         L.ntt_get_tables.argtypes = [ctypes.c_int] + [_u32p] * 5
         for nm in ("poly_ntt", "poly_invntt"):
             getattr(L, nm).argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
-        for nm in ("poly_ntt_oop", "poly_invntt_oop"):
+        for nm in ("poly_ntt_oop", "poly_invntt_oop", "poly_bitrev_copy"):
             getattr(L, nm).argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
         for nm in ("poly_mul", "poly_mul_ntt", "poly_pointwise"):
             getattr(L, nm).argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, _vp]
@@ -198,6 +198,17 @@ def poly_invntt_oop(out, inp, param_set, stream=None):
         raise ValueError("out/in batch mismatch")
     _check(lib().poly_invntt_oop(out.data_ptr(), inp.data_ptr(), b, _ps(param_set), _stream(stream)),
            "poly_invntt_oop")
+    return out
+
+
+def poly_bitrev_copy(out, inp, param_set, stream=None):
+    """out[b, t] = inp[b, brv(t)] (bit_reverse_copy_tbl_gpu); out may be inp."""
+    n = param_info(param_set)["n"]
+    b = _batch(inp, n)
+    if _batch(out, n) != b:
+        raise ValueError("out/in batch mismatch")
+    _check(lib().poly_bitrev_copy(out.data_ptr(), inp.data_ptr(), b, _ps(param_set), _stream(stream)),
+           "poly_bitrev_copy")
     return out
 
 

@@ -121,6 +121,15 @@ def poly_invntt_ct(X, param_set):
     return y.reshape(np.shape(X))
 
 
+def bit_reverse_copy(x, param_set):
+    """bit_reverse_copy (NTT.cu:81-91) restated in C: out[t] = in[brv(t)]"""
+    n = params(param_set)["n"]
+    x = _batched(x, n)
+    y = np.zeros_like(x)
+    lib().oracle_bit_reverse_copy(_ptr(x), _ptr(y), x.size // n, _ps(param_set))
+    return y
+
+
 def poly_mul(a, b, param_set):
     n = params(param_set)["n"]
     a = _batched(a, n)

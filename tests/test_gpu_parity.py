@@ -224,6 +224,10 @@ def test_host_driver_kat(ps):
     r = subprocess.run([exe, "-speedgpu", "9", "-param", ps, "-batch", "1000", "-r", "5"], capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0 and "Identical." in r.stdout, r.stdout + r.stderr
+    for opt, batch in (("10", "5000"), ("11", "7")):   # host pipeline (2 chunks at n=1024), Nussbaumer mod 2^32-1
+        r = subprocess.run([exe, "-speedgpu", opt, "-param", ps, "-batch", batch], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0 and "Identical." in r.stdout, r.stdout + r.stderr
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
@@ -244,3 +248,20 @@ def test_poly_mul_ntt_domain(ntt, oracle, dev, ps, batch):
     bl = (oracle.poly_ntt(b, ps).astype(np.uint64) + q).astype(np.uint32)
     ntt.poly_mul_ntt(ta, ta, _dev(ntt, bl, dev), ps)
     assert np.array_equal(_u32(ntt, ta), want)
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+@pytest.mark.parametrize("batch", [1, 3, 130])
+def test_bitrev_copy(ntt, oracle, dev, ps, batch):
+    """poly_bitrev_copy == bit_reverse_copy_tbl_gpu (NTT.cu:487-492) on arbitrary 32-bit words."""
+    n = ntt.param_info(ps)["n"]
+    rng = np.random.default_rng(batch + n)
+    x = rng.integers(0, 1 << 32, (batch, n), dtype=np.uint64).astype(np.uint32)
+    want = x[:, ntt.tables(ps)["bitrev_tbl"]]
+    assert np.array_equal(want, oracle.bit_reverse_copy(x, ps))
+    t = _dev(ntt, x, dev)
+    o = torch.empty_like(t)
+    ntt.poly_bitrev_copy(o, t, ps)
+    assert np.array_equal(_u32(ntt, o), want)
+    ntt.poly_bitrev_copy(t, t, ps)          # in place
+    assert np.array_equal(_u32(ntt, t), want)
