@@ -124,14 +124,30 @@ __device__ __forceinline__ void ct_bfly(uint32_t &x, uint32_t &y, uint32_t wn, u
     y = a + tn + 2 * Q;
 }
 
+// Signed Shoup product: d is read as a signed 32-bit value with |d| < 2^31,
+// the twiddle is stored centred, ws in (-q/2, q/2], with wps = floor(ws 2^32 / q)
+// (a signed 32-bit value).  |d ws / q - d wps / 2^32| < 1/2, so with the
+// rounded quotient minus one, e = floor((d wps - 2^31) / 2^32),
+//   d ws - e q  lies in (0, 2q)  and is congruent to d * ws.
+// Three mul-class instructions (v_mad_i64_i32, v_mul_lo_u32, v_mad_u64_u32),
+// like shoup_mul, but d = x - y needs no +2q bias.
 template <uint32_t Q>
-__device__ __forceinline__ void gs_bfly(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp)
+__device__ __forceinline__ uint32_t sshoup_mul(uint32_t d, uint32_t ws, uint32_t wps)
+{
+    const uint32_t e = (uint32_t)(((int64_t)(int32_t)d * (int32_t)wps - 0x80000000ll) >> 32);
+    return madlo32(e, 0u - Q, mullo32(d, ws));
+}
+
+// GS butterfly, inputs in [0,2q): x' = (x+y) mod 2q, y' = (x-y) w in [0,2q).
+// 7 VALU: v_add, v_sub, v_min, v_sub, then the three of sshoup_mul.
+template <uint32_t Q>
+__device__ __forceinline__ void gs_bfly(uint32_t &x, uint32_t &y, uint32_t ws, uint32_t wps)
 {
     uint32_t s = x + y;                          // [0,4q)
     s = umin(s, s - 2 * Q);
-    const uint32_t d = x - y + 2 * Q;            // (0,4q)
+    const uint32_t d = x - y;                    // (-2q, 2q) as a signed value
     x = s;
-    y = shoup_mul<Q>(d, w, wp);
+    y = sshoup_mul<Q>(d, ws, wps);
 }
 
 // Montgomery product, a,b in [0,2q): returns a*b*2^-32 mod q in [0,2q)
@@ -411,14 +427,15 @@ __device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const u
             }
         }
     }
-    constexpr uint32_t S0P = cshoup(S0, P::Q), S1P = cshoup(S1, P::Q);
+    constexpr uint32_t S0P = cshoup(S0, P::Q);
+    constexpr TwPair S1S = csigned_tw(S1, P::Q);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint32_t x = r[j], y = r[j + 16];
         const uint32_t s = x + y;              // [0,4q)
-        const uint32_t d = x - y + 2 * P::Q;   // (0,4q)
+        const uint32_t d = x - y;              // (-2q, 2q), signed
         uint32_t a = shoup_mul<P::Q>(s, S0, S0P);
-        uint32_t b = shoup_mul<P::Q>(d, S1, S1P);
+        uint32_t b = sshoup_mul<P::Q>(d, S1S.x, S1S.y);
         r[j] = umin(a, a - P::Q);
         r[j + 16] = umin(b, b - P::Q);
         emit(j, r[j]);
@@ -954,8 +971,15 @@ int upload_tables(int dev)
     for (const auto &s : syms) {
         const Tables &t = cpu_tables(s.ps);
         std::vector<uint32_t> v = s.inv ? t.inv : t.fwd;
-        if (!s.inv)   // device forward table holds (2^32 - w, w'): see ct_bfly
-            for (size_t k = 0; k < v.size(); k += 2) v[k] = 0u - v[k];
+        for (size_t k = 0; k < v.size(); k += 2) {
+            if (s.inv) {   // device inverse table holds the centred (ws, ws'): see sshoup_mul
+                const TwPair c = csigned_tw(v[k], param_set(s.ps)->q);
+                v[k] = c.x;
+                v[k + 1] = c.y;
+            } else {       // device forward table holds (2^32 - w, w'): see ct_bfly
+                v[k] = 0u - v[k];
+            }
+        }
         hipError_t e = hipMemcpyToSymbol(s.sym, v.data(), v.size() * 4, 0, hipMemcpyHostToDevice);
         if (e != hipSuccess) { t_last_hip = (int)e; return NTT_ERR_HIP; }
     }
@@ -971,8 +995,14 @@ int upload_tables(int dev)
                 std::vector<uint32_t> &o = img[ps][inv];
                 o.assign(TW2_WORDS, 0);
                 auto put = [&](int slot, uint32_t k) {
-                    o[2 * slot] = inv ? tw[2 * k] : 0u - tw[2 * k];   // forward stored negated (ct_bfly)
-                    o[2 * slot + 1] = tw[2 * k + 1];
+                    if (inv) {   // inverse stored centred (sshoup_mul)
+                        const TwPair c = csigned_tw(tw[2 * k], p.q);
+                        o[2 * slot] = c.x;
+                        o[2 * slot + 1] = c.y;
+                    } else {     // forward stored negated (ct_bfly)
+                        o[2 * slot] = 0u - tw[2 * k];
+                        o[2 * slot + 1] = tw[2 * k + 1];
+                    }
                 };
                 for (int e = 0; e < TW2_ENTRIES; e++) {
                     const int b = e < 1 ? 4 : e < 3 ? 3 : e < 7 ? 2 : e < 15 ? 1 : 0;

@@ -19,6 +19,17 @@ constexpr uint32_t cpow(uint64_t b, uint64_t e, uint64_t q)
     return (uint32_t)r;
 }
 constexpr uint32_t cshoup(uint32_t w, uint32_t q) { return (uint32_t)(((uint64_t)w << 32) / q); }
+// Centred twiddle for the signed Shoup product (sshoup_mul): ws = w or w - q,
+// whichever lies in (-q/2, q/2], and wps = floor(ws 2^32 / q), both as the
+// bit patterns of signed 32-bit values.
+struct TwPair { uint32_t x, y; };
+constexpr TwPair csigned_tw(uint32_t w, uint32_t q)
+{
+    const int64_t ws = w <= q / 2 ? (int64_t)w : (int64_t)w - (int64_t)q;
+    const int64_t num = ws * ((int64_t)1 << 32);
+    const int64_t wps = num >= 0 ? num / (int64_t)q : -((-num + (int64_t)q - 1) / (int64_t)q);
+    return {(uint32_t)(int32_t)ws, (uint32_t)(int32_t)wps};
+}
 constexpr uint32_t cqinv_neg(uint32_t q)
 {
     uint32_t inv = q;

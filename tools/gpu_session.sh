@@ -16,7 +16,7 @@ for step in "$@"; do
     case $step in
         valu)   run valu 60 ./ntt-gpu-qtesla_amd/bin/valu_rates ;;
         smoke)  run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        pytest) run pytest 600 python -m pytest tests -x -q -m gpu ;;
+        pytest) run pytest 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread ;;
         pytestq) run pytest 600 python -m pytest tests -x -q -m "gpu and not slow" ;;
         bench)  run bench 400 python bench.py --steps 10 --warmup 2 --cpu-seconds 8 ;;
         benchq) run bench 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
@@ -29,6 +29,9 @@ for step in "$@"; do
              run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 tools/variants.py --only fwd_full,inv_full,torch_copy --rounds 2 &&
              run pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sq -o run -- python3 tools/variants.py --only fwd_full,inv_full --rounds 2 ;;
         ab) for f in ntt-gpu-qtesla_amd/lib/ab/*.so; do b=$(basename $f .so); NTT_AMD_LIB=$PWD/$f run ab_$b 200 python tools/variants.py --rounds 5 --only fwd_full,inv_full,fwd_alu,inv_alu,fwd_mem,inv_mem || exit 1; done ;;
+        abx) run abx_p3 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --ops fwd,inv,mul,mulntt --inplace --rounds 7 &&
+             run abx_p1 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param p-I --ops fwd,inv,mul --inplace --rounds 7 &&
+             run abx_p1s 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param p-I --batch 65536 --ops fwd,inv --inplace --rounds 21 ;;
         cycles) run cycles 120 ./ntt-gpu-qtesla_amd/bin/valu_cycles ;;
         clock) run pmc_clock 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/pmc_clock -o run -- python3 tools/variants.py --rounds 2 ;;
         bocc) run bocc 120 ./ntt-gpu-qtesla_amd/bin/bfly_occupancy ;;
