@@ -43,9 +43,10 @@ extern "C" {
 #define NTT_OK 0
 #define NTT_ERR_PARAM (-1)   /* unknown param_set                              */
 #define NTT_ERR_NULL (-2)    /* NULL device pointer with batch > 0             */
-#define NTT_ERR_ALIGN (-3)   /* device pointer not 4-byte aligned              */
+#define NTT_ERR_ALIGN (-3)   /* device pointer not 4-byte aligned (16-byte for  */
+                             /* poly_pointwise and poly_mul_nussbaumer)        */
 #define NTT_ERR_HIP (-4)     /* HIP runtime / launch error (ntt_last_hip_error)*/
-#define NTT_ERR_SIZE (-5)    /* batch too large (batch*n must fit in 2^40)     */
+#define NTT_ERR_SIZE (-5)    /* batch too large (at most 2^31 - 1 polynomials) */
 #define NTT_ERR_ALIAS (-6)   /* forbidden partial overlap of in/out buffers    */
 
 /* Parameter query: any out pointer may be NULL.
@@ -84,6 +85,22 @@ int poly_ntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch,
 int poly_invntt_oop(uint32_t *d_out, const uint32_t *d_in, size_t batch,
                     int param_set, void *stream);
 
+/* Transforms with the NTT domain in bit-reversed order (out of place; d_out
+ * may equal d_in, partial overlap rejected), for callers that keep the
+ * reference's CT-CT ordering:
+ *   poly_ntt_bitrev:    out[t] = X[brv(t)]  (= poly_ntt then poly_bitrev_copy)
+ *   poly_invntt_bitrev: input in[t] = X[brv(t)], natural-order output; this
+ *     is the CT inverse on bit-reversed input radix2INTT_gpu0 x5 + gpu1 x4 +
+ *     gpu2 with its x invPhi (NTT.cu:2240-2249, kernels :1374-1433) -- 10
+ *     launches -> 1; poly_bitrev_copy then poly_invntt_bitrev = poly_invntt.
+ * Each costs one more LDS transpose per polynomial than the natural-order
+ * transform (the bit-reversed side is not lane-contiguous in the pass-2
+ * register layout). */
+int poly_ntt_bitrev(uint32_t *d_out, const uint32_t *d_in, size_t batch,
+                    int param_set, void *stream);
+int poly_invntt_bitrev(uint32_t *d_out, const uint32_t *d_in, size_t batch,
+                       int param_set, void *stream);
+
 /* Bit-reversal permutation, out[b*n + t] = in[b*n + brv(t)] (log2 n bits),
  * any 32-bit words.  Replaces bit_reverse_copy_tbl_gpu (NTT.cu:487-492), used
  * by the CT-CT pipeline (:2239) to feed radix2INTT with bit-reversed input.
@@ -117,14 +134,15 @@ int poly_mul_ntt(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_bhat,
  *                      read as zero, outputs canonical in [0, 2^32 - 1).
  *   ring NTT_RING_Q:   coefficients mod param_set's q, inputs < 2q, outputs
  *                      canonical -- bit-identical to poly_mul.
- * d_c may alias d_a or d_b. */
+ * d_c may alias d_a or d_b.  All three pointers must be 16-byte aligned. */
 #define NTT_RING_Q 0
 #define NTT_RING_M32 1
 int poly_mul_nussbaumer(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,
                         size_t batch, int param_set, int ring, void *stream);
 
 /* Pointwise product c[i] = a[i] * b[i] mod q over batch*n coefficients.
- * Replaces pointwise_mult (NTT.cu:1155-1160). */
+ * Replaces pointwise_mult (NTT.cu:1155-1160).  Inputs < 2q, canonical output;
+ * all three pointers must be 16-byte aligned; d_c may alias d_a or d_b. */
 int poly_pointwise(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,
                    size_t batch, int param_set, void *stream);
 
@@ -166,7 +184,17 @@ void ntt_host_free(void *p);
 int ntt_last_hip_error(void);
 const char *ntt_strerror(int code);
 
-/* Library / kernel description for reports: writes at most len bytes. */
+/* Tuning: work loop of the transforms (poly_ntt / poly_invntt and their _oop
+ * forms).  -1 (default) = automatic: LDS-DMA prefetch of the next polynomial
+ * for launches of at most two workgroup rounds (small batches, where all
+ * waves would otherwise load, compute and store in phase), the plain loop
+ * above that; 0 = never; 1 = always.  Results are identical either way.
+ * Process-wide; the initial value may be set by the environment variable
+ * QTESLA_NTT_PREFETCH=0|1.  Returns the previous policy, or NTT_ERR_PARAM. */
+int ntt_set_prefetch(int policy);
+
+/* Library / kernel description for reports, ending in "src=<16 hex>" (a hash
+ * of the library sources): writes at most len bytes, returns the length. */
 int ntt_build_info(char *buf, size_t len);
 
 #ifdef __cplusplus

@@ -1,0 +1,80 @@
+// dev_tables.hpp -- host-side construction and upload of the device twiddle
+// tables of ntt_device.hpp, in the kernels' conventions:
+//   forward (w, w') stored as (2^32 - w, w')          (ct_bfly)
+//   inverse (w, w') stored centred as (ws, ws')        (sshoup_mul)
+//   per-workgroup LDS images of the pass-2 lane twiddles + the bit-5 table
+// Included by the translation unit that owns the __constant__ / __device__
+// symbols (one per shared object).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "ntt_device.hpp"
+#include "params.hpp"
+
+namespace qntt {
+
+// (w, w') of twiddle index k of one direction, in the device convention
+inline void dev_pair(const ParamSet &p, const Tables &t, bool inv, uint32_t k, uint32_t &w, uint32_t &wp)
+{
+    const std::vector<uint32_t> &tw = inv ? t.inv : t.fwd;
+    if (inv) {
+        const TwPair c = csigned_tw(tw[2 * k], p.q);
+        w = c.x;
+        wp = c.y;
+    } else {
+        w = 0u - tw[2 * k];
+        wp = tw[2 * k + 1];
+    }
+}
+
+// __constant__ table: n pairs, index k
+inline std::vector<uint32_t> dev_const_table(const ParamSet &p, const Tables &t, bool inv)
+{
+    std::vector<uint32_t> v(2 * p.n);
+    for (uint32_t k = 0; k < p.n; k++) dev_pair(p, t, inv, k, v[2 * k], v[2 * k + 1]);
+    return v;
+}
+
+// LDS image (fill_tw2): entry e of stage bit b = tw2_b(e), lane t holds twiddle
+// k = 2^(logn-1-b) + (Lp << (4-b)) + m with Lp = bitrev(lane) (see Lane);
+// then the 32 bit-5 twiddles k = 32 + i.
+inline std::vector<uint32_t> dev_tw2_image(const ParamSet &p, const Tables &t, bool inv)
+{
+    std::vector<uint32_t> o(TW2_WORDS, 0);
+    auto put = [&](int slot, uint32_t k) { dev_pair(p, t, inv, k, o[2 * slot], o[2 * slot + 1]); };
+    for (int e = 0; e < TW2_ENTRIES; e++) {
+        const int b = e < 1 ? 4 : e < 3 ? 3 : e < 7 ? 2 : e < 15 ? 1 : 0;
+        const uint32_t m = e - ((1u << (4 - b)) - 1);
+        for (uint32_t lane = 0; lane < 64; lane++) {
+            const uint32_t Lp = p.logn == 11 ? bitrev(lane, 6) : bitrev(lane & 31, 5);
+            put(e * 64 + lane, (1u << (p.logn - 1 - b)) + (Lp << (4 - b)) + m);
+        }
+    }
+    for (int i = 0; i < 32; i++) put(TW2_ENTRIES * 64 + i, 32u + i);
+    return o;
+}
+
+// Upload every table of the three parameter sets to the current device.
+inline hipError_t upload_device_tables(const Tables *tabs /* [3] */)
+{
+    const void *syms[3][2] = {{HIP_SYMBOL(c_fwd0), HIP_SYMBOL(c_inv0)},
+                              {HIP_SYMBOL(c_fwd1), HIP_SYMBOL(c_inv1)},
+                              {HIP_SYMBOL(c_fwd2), HIP_SYMBOL(c_inv2)}};
+    for (int ps = 0; ps < 3; ps++)
+        for (int inv = 0; inv < 2; inv++) {
+            const ParamSet &p = *param_set(ps);
+            const std::vector<uint32_t> c = dev_const_table(p, tabs[ps], inv != 0);
+            hipError_t e = hipMemcpyToSymbol(syms[ps][inv], c.data(), c.size() * 4, 0, hipMemcpyHostToDevice);
+            if (e != hipSuccess) return e;
+            const std::vector<uint32_t> img = dev_tw2_image(p, tabs[ps], inv != 0);
+            e = hipMemcpyToSymbol(HIP_SYMBOL(g_tw2img), img.data(), TW2_WORDS * 4,
+                                  (size_t)(ps * 2 + inv) * TW2_WORDS * 4, hipMemcpyHostToDevice);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
+}  // namespace qntt

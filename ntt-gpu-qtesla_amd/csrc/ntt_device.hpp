@@ -1,0 +1,816 @@
+// ntt_device.hpp -- gfx950 (CDNA4) device code of the batched negacyclic NTT:
+// arithmetic, register/LDS geometry, transform passes and the kernel templates.
+// Included by exactly one translation unit per shared object (csrc/ntt_kernels.hip
+// for the product library, tools/ntt_diag.hip for the diagnostic one).
+//
+// Replaces the reference's 10-34 per-stage launches per batch (NTT.cu:2388-2425)
+// with one launch per operation.  Geometry:
+//
+//   * one wave owns one n=2048 polynomial, or two n=1024 polynomials (one per
+//     32-lane half); every lane holds 32 coefficients in VGPRs;
+//   * pass 1: register layout pos = lane + S*j (S = 64 or 32, j = 0..31); the
+//     five stages on pos bits [LOGN-5, LOGN-1] are in-register radix-2
+//     butterflies with wave-uniform twiddles (scalar loads from __constant__);
+//   * n = 2048 only: the stage on pos bit 5 pairs lanes l and l^32 and runs on
+//     v_permlane32_swap (no LDS);
+//   * one wave-private LDS transpose (conflict-free XOR swizzle, 32 x ds_write_b32
+//     + 8 x ds_read_b128 per lane, no s_barrier) to layout pos = 32*Lp + j;
+//   * pass 2: the five stages on pos bits [0,4] in registers with per-lane
+//     twiddles read from the workgroup's LDS table;
+//   * the forward's output is bit-reversed in registers and is written in
+//     natural order directly: for fixed j the lanes cover one contiguous run.
+//
+// Arithmetic: Harvey lazy butterflies with Shoup (precomputed-quotient
+// Barrett) multiplication, q < 2^30 so 4q < 2^32:
+//   CT: x in [0,4q) -> x' = x mod 2q;  t = y*w mod q in [0,2q);
+//       (x'+t, x'-t+2q) in [0,4q)^2                             (7 VALU)
+//   GS: (x+y reduced to [0,2q), (x-y)*w by a signed Shoup product in [0,2q))
+//                                                               (7 VALU)
+// Outputs are reduced to canonical [0,q) before they are stored.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "pset.hpp"
+
+namespace qntt {
+
+// twiddles (w, w'), index k in [0, n): fwd = psi^brv(k) stored negated,
+// inv = psi^-brv(k) stored centred (see ct_bfly / sshoup_mul)
+__constant__ uint2 c_fwd0[1024];
+__constant__ uint2 c_inv0[1024];
+__constant__ uint2 c_fwd1[1024];
+__constant__ uint2 c_inv1[1024];
+__constant__ uint2 c_fwd2[2048];
+__constant__ uint2 c_inv2[2048];
+
+// ------------------------------------------------------------------------
+// modular arithmetic (NTT.cu:379-470 barrett_red/_addModP/_subModP, restated)
+// ------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+// low word of a*b + c (one v_mad_u64_u32)
+__device__ __forceinline__ uint32_t madlo32(uint32_t a, uint32_t b, uint32_t c)
+{
+    return (uint32_t)((uint64_t)a * b + c);
+}
+
+template <uint32_t Q>
+__device__ __forceinline__ uint32_t shoup_mul(uint32_t a, uint32_t w, uint32_t wp)
+{
+    // a < 2^32, w < q, wp = floor(w 2^32 / q)  ->  result == a*w mod q, in [0, 2q)
+    const uint32_t qe = __umulhi(a, wp);
+    return madlo32(qe, 0u - Q, a * w);
+}
+
+// Signed Shoup product: d is read as a signed 32-bit value with |d| < 2^31,
+// the twiddle is stored centred, ws in (-q/2, q/2], with wps = floor(ws 2^32 / q)
+// (a signed 32-bit value).  |d ws / q - d wps / 2^32| < 1/2, so with the
+// rounded quotient minus one, e = floor((d wps - 2^31) / 2^32),
+//   d ws - e q  lies in (0, 2q)  and is congruent to d * ws.
+// Three mul-class instructions (v_mad_i64_i32, v_mul_lo_u32, v_mad_u64_u32),
+// like shoup_mul, but d = x - y needs no +2q bias.
+template <uint32_t Q>
+__device__ __forceinline__ uint32_t sshoup_mul(uint32_t d, uint32_t ws, uint32_t wps)
+{
+    const uint32_t e = (uint32_t)(((int64_t)(int32_t)d * (int32_t)wps - 0x80000000ll) >> 32);
+    return madlo32(e, 0u - Q, d * ws);
+}
+
+// Forward twiddles are stored NEGATED on the device (wn = 2^32 - w, Shoup
+// companion wp of w): the multiply-add then yields -t directly, so both outputs
+// cost one instruction each (v_sub, v_add3):  x' = a + t,  y' = a - t + 2q.
+template <uint32_t Q, bool REDUCE = true>
+__device__ __forceinline__ void ct_bfly(uint32_t &x, uint32_t &y, uint32_t wn, uint32_t wp)
+{
+    const uint32_t a = REDUCE ? umin(x, x - 2 * Q) : x;   // [0,4q) -> [0,2q)
+    const uint32_t qe = __umulhi(y, wp);
+    const uint32_t tn = madlo32(qe, Q, y * wn);           // -t, t in [0,2q)
+    x = a - tn;
+    y = a + tn + 2 * Q;
+}
+
+// GS butterfly, inputs in [0,2q): x' = (x+y) mod 2q, y' = (x-y) w in [0,2q).
+// 7 VALU: v_add, v_sub, v_min, v_sub, then the three of sshoup_mul.
+template <uint32_t Q>
+__device__ __forceinline__ void gs_bfly(uint32_t &x, uint32_t &y, uint32_t ws, uint32_t wps)
+{
+    uint32_t s = x + y;   // [0,4q)
+    s = umin(s, s - 2 * Q);
+    const uint32_t d = x - y;   // (-2q, 2q) as a signed value
+    x = s;
+    y = sshoup_mul<Q>(d, ws, wps);
+}
+
+// Montgomery product, a,b in [0,2q): returns a*b*2^-32 mod q in [0,2q)
+template <class P>
+__device__ __forceinline__ uint32_t mont_mul(uint32_t a, uint32_t b)
+{
+    const uint32_t lo = a * b;
+    const uint32_t hi = __umulhi(a, b);
+    const uint32_t m = lo * P::QNEG;
+    return hi + __umulhi(m, P::Q) + (lo != 0u ? 1u : 0u);
+}
+
+// [0,4q) -> canonical [0,q)
+template <class P>
+__device__ __forceinline__ uint32_t canon4(uint32_t x)
+{
+    x = umin(x, x - P::Q2);
+    return umin(x, x - P::Q);
+}
+
+// ------------------------------------------------------------------------
+// per-lane geometry and the wave-private LDS transpose
+// ------------------------------------------------------------------------
+// XOR swizzle of the transpose buffer (hi = pos >> 5):
+//   phys(pos) = pos ^ (pos8 << 2) ^ (pos9 << 3) ^ ((pos7 ^ pos10) << 4) ^ (pos7 << 5)
+// Bijective; conflict-free for ds_write_b32 / ds_read_b32 in the pass-1
+// layouts and ds_read_b128 / ds_write_b128 in the bit-reversed pass-2
+// layout (tests/test_lds_layout.py, gfx950 lane-group bank model).
+__host__ __device__ constexpr uint32_t xm_of(uint32_t hi)   // XOR on pos bits 2..4
+{
+    return (((hi >> 3) & 1) << 2) | (((hi >> 4) & 1) << 3) | ((((hi >> 2) ^ (hi >> 5)) & 1) << 4);
+}
+
+template <class P>
+struct Lane {
+    static constexpr bool BIG = (P::LOGN == 11);   // one poly per wave
+    static constexpr uint32_t S = BIG ? 64 : 32;   // pass-1 stride
+    static constexpr uint32_t UPW = BIG ? 1 : 2;   // polys per wave unit
+    uint32_t lane, h, Lp;
+    uint32_t wlo, woff;    // pass-1 LDS write/read (b32) address parts
+    uint32_t rbase, rxm;   // pass-2 LDS read/write (b128) address parts
+    uint32_t brl;          // lane index within its poly: pass-1 column, and bitrev(Lp)
+
+    __device__ __forceinline__ Lane()
+    {
+        lane = threadIdx.x & 63;
+        h = lane >> 5;
+        // pass-2 row of this lane: Lp = bitrev(lane).  Then the bit-reversed
+        // side of each transform (forward store, inverse load) addresses
+        // brv5(j) * S + brv(Lp) = brv5(j) * S + lane: lane-contiguous 128/256-B runs.
+        Lp = BIG ? (__builtin_bitreverse32(lane) >> 26) : (__builtin_bitreverse32(lane & 31) >> 27);
+        wlo = lane & 31;
+        woff = BIG ? 64 * h : 1024 * h;
+        rxm = xm_of(Lp);
+        rbase = 32 * (Lp ^ ((Lp >> 2) & 1)) + (BIG ? 0u : 1024 * h);
+        brl = BIG ? lane : (lane & 31);
+    }
+    // index of this lane's polynomial in wave unit u
+    __device__ __forceinline__ uint32_t poly(uint32_t u) const { return u * UPW + (BIG ? 0u : h); }
+};
+
+// pos>>5 of register j in the pass-1 layout (n=2048: after the bit-5 swap)
+template <class P>
+__host__ __device__ constexpr uint32_t hi_of(int j)
+{
+    return P::LOGN == 11 ? (uint32_t)((j & 1) + 4 * (j >> 1)) : (uint32_t)j;
+}
+
+// Word offset, relative to the lane's `brl` column of its polynomial, of
+// register j in the pass-1 arrangement that the transposes use (n = 2048: the
+// post-swap arrangement pos = l5 + 32 e + 64 h + 128 m for j = 2m + e, i.e.
+// two 128-B runs per instruction; n = 1024: pos = l5 + 32 j).
+template <class P>
+__host__ __device__ constexpr uint32_t p1s_off(int j)
+{
+    return P::LOGN == 11 ? (uint32_t)(32 * (j & 1) + 128 * (j >> 1)) : (uint32_t)(32 * j);
+}
+
+template <class P>
+__device__ __forceinline__ uint32_t p1_addr(const Lane<P> &L, int j)
+{
+    const uint32_t hj = hi_of<P>(j);   // the lane part of hi (n = 2048: 2h) enters neither XOR term
+    return (L.wlo ^ xm_of(hj)) + 32 * (hj ^ ((hj >> 2) & 1)) + L.woff;
+}
+
+// LDS operations of one wave complete in issue order, so the wave-private
+// transposes need no s_barrier; this only keeps the compiler from moving
+// accesses across the phase boundaries.
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+// A wave-uniform zero the compiler cannot see through.  Adding it to the
+// index of a uniform twiddle load keeps that load an s_load inside the
+// work loop instead of letting LICM hoist all ~126 twiddle words into
+// registers (which cost 2-3 waves/SIMD of occupancy).
+__device__ __forceinline__ uint32_t opaque_zero()
+{
+    uint32_t z = 0;
+    asm volatile("" : "+s"(z));
+    return z;
+}
+
+constexpr int XPOSE_WORDS = 2048;   // per-wave transpose buffer (8 KiB)
+
+// pass-1 arrangement (registers, post-swap for n=2048) -> pass-2 layout
+template <class P>
+__device__ __forceinline__ void lds_p1_to_p2(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
+{
+#pragma unroll
+    for (int j = 0; j < 32; ++j) buf[p1_addr<P>(L, j)] = r[j];
+    compiler_fence();
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(buf + L.rbase + ((4u * c) ^ L.rxm));
+        r[4 * c + 0] = v.x;
+        r[4 * c + 1] = v.y;
+        r[4 * c + 2] = v.z;
+        r[4 * c + 3] = v.w;
+    }
+    compiler_fence();
+}
+
+// pass-2 layout -> pass-1 arrangement (n=2048: the post-swap arrangement)
+template <class P>
+__device__ __forceinline__ void lds_p2_to_p1(uint32_t (&r)[32], uint32_t *buf, const Lane<P> &L)
+{
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        *reinterpret_cast<uint4 *>(buf + L.rbase + ((4u * c) ^ L.rxm)) =
+            make_uint4(r[4 * c + 0], r[4 * c + 1], r[4 * c + 2], r[4 * c + 3]);
+    compiler_fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) r[j] = buf[p1_addr<P>(L, j)];
+    compiler_fence();
+}
+
+__device__ __forceinline__ constexpr uint32_t brv5(int j)
+{
+    return (uint32_t)(((j & 1) << 4) | ((j & 2) << 2) | (j & 4) | ((j & 8) >> 2) | ((j & 16) >> 4));
+}
+
+// ------------------------------------------------------------------------
+// twiddle access
+// ------------------------------------------------------------------------
+// Table base + an opaque wave-uniform zero: every uniform twiddle read below
+// becomes an s_load_dwordx{2,8,16} with an immediate offset, re-issued per
+// work unit instead of ~126 hoisted words pinning registers.
+template <int PS, bool INV>
+__device__ __forceinline__ const uint2 *tw_base()
+{
+    const uint32_t z = opaque_zero();
+    if constexpr (PS == 0) return (INV ? c_inv0 : c_fwd0) + z;
+    else if constexpr (PS == 1) return (INV ? c_inv1 : c_fwd1) + z;
+    else return (INV ? c_inv2 : c_fwd2) + z;
+}
+
+// Per-lane pass-2 twiddles live in a per-workgroup LDS table, lane-major
+// (entry e, lane t) so a ds_read_b64 by 64 lanes is conflict-free:
+//   e = 2^(4-b) - 1 + m for stage bit b,  k = 2^(LOGN-1-b) + (Lp << (4-b)) + m
+constexpr int TW2_ENTRIES = 31;
+constexpr int TW2_WORDS = TW2_ENTRIES * 64 * 2 + 64;   // 15.5 KiB + the 32-entry bit-5 table
+constexpr int TW2_VEC4 = TW2_WORDS / 4;                // 1008 uint4
+
+// Host-built images of the per-workgroup LDS twiddle table (lane-major
+// pass-2 entries + the 32-entry bit-5 table), one per (param set, direction):
+// the workgroup prologue is then one coalesced 16 KiB copy with one wait.
+__device__ uint4 g_tw2img[3][2][TW2_VEC4];
+
+template <int PS, bool INV, int NT>
+__device__ __forceinline__ void fill_tw2(uint2 *tab)
+{
+    const uint4 *src = g_tw2img[PS][INV ? 1 : 0];
+    uint4 *dst = reinterpret_cast<uint4 *>(tab);
+    constexpr int ITER = (TW2_VEC4 + NT - 1) / NT;
+    uint4 v[ITER];
+#pragma unroll
+    for (int k = 0; k < ITER; ++k) {
+        const int i = threadIdx.x + k * NT;
+        if (i < TW2_VEC4) v[k] = src[i];
+    }
+#pragma unroll
+    for (int k = 0; k < ITER; ++k) {
+        const int i = threadIdx.x + k * NT;
+        if (i < TW2_VEC4) dst[i] = v[k];
+    }
+}
+
+// ------------------------------------------------------------------------
+// transform passes
+// ------------------------------------------------------------------------
+// forward pass 1: CT stages on pos bits LOGN-1 .. LOGN-5 (j bits 4..0),
+// twiddle index k = 2^s + (j >> (5-s)) -- wave-uniform.
+template <int PS, class P>
+__device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw)
+{
+    const uint2 *tw = tw_base<PS, false>();
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const int hh = 16 >> s;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const uint2 w = tw[(1u << s) + (uint32_t)(j >> (5 - s))];
+                if (s == 0) ct_bfly<P::Q, false>(r[j], r[j + hh], w.x, w.y);   // inputs < 2q
+                else ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+            }
+        }
+    }
+    if constexpr (P::LOGN == 11) {
+        // pos bit 5 pairs lanes l, l^32: exchange halves, butterfly, keep the
+        // swapped arrangement (p1_addr accounts for it)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
+            r[2 * m] = pr[0];
+            r[2 * m + 1] = pr[1];
+            const uint2 w = sw[2 * m + h];   // k = 32 + 2m + h
+            ct_bfly<P::Q>(r[2 * m], r[2 * m + 1], w.x, w.y);
+        }
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void fwd_pass2(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
+{
+#pragma unroll
+    for (int b = 4; b >= 0; --b) {
+        const int hh = 1 << b;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
+                const uint2 w = tab[e * 64 + lane];
+                ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+            }
+        }
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
+{
+#pragma unroll
+    for (int b = 0; b <= 4; ++b) {
+        const int hh = 1 << b;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
+                const uint2 w = tab[e * 64 + lane];
+                gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+            }
+        }
+    }
+}
+
+struct NoEmit {
+    __device__ __forceinline__ void operator()(int, uint32_t) const {}
+};
+
+// inverse pass 1: (n=2048) GS on pos bit 5 + swap back, then GS stages on pos
+// bits LOGN-5 .. LOGN-1 (j bits 0..4); the last one carries the n^-1 scaling
+// (times the S0 / S1 constants), output canonical.  `emit(j, v)` is called
+// with each final output as soon as it is computed (the kernels store from
+// there, so the 32 stores interleave with the last stage instead of queueing
+// behind it as one tail).
+template <int PS, class P, uint32_t S0, uint32_t S1, class Emit = NoEmit>
+__device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw, const Emit &emit = Emit())
+{
+    const uint2 *tw = tw_base<PS, true>();
+    if constexpr (P::LOGN == 11) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const uint2 w = sw[2 * m + h];
+            gs_bfly<P::Q>(r[2 * m], r[2 * m + 1], w.x, w.y);
+            const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
+            r[2 * m] = pr[0];
+            r[2 * m + 1] = pr[1];
+        }
+    }
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+        const int hh = 1 << jb;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const uint2 w = tw[(16u >> jb) + (uint32_t)(j >> (jb + 1))];
+                gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+            }
+        }
+    }
+    constexpr uint32_t S0P = cshoup(S0, P::Q);
+    constexpr TwPair S1S = csigned_tw(S1, P::Q);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t x = r[j], y = r[j + 16];
+        const uint32_t s = x + y;   // [0,4q)
+        const uint32_t d = x - y;   // (-2q, 2q), signed
+        const uint32_t a = shoup_mul<P::Q>(s, S0, S0P);
+        const uint32_t b = sshoup_mul<P::Q>(d, S1S.x, S1S.y);
+        r[j] = umin(a, a - P::Q);
+        r[j + 16] = umin(b, b - P::Q);
+        emit(j, r[j]);
+        emit(j + 16, r[j + 16]);
+    }
+}
+
+// ------------------------------------------------------------------------
+// global memory access
+// ------------------------------------------------------------------------
+// Output stores are nontemporal (streamed once, never re-read by the kernel);
+// input loads too (read once): with nt stores, in place -4.5 % fwd / -2.1 %
+// inv (profiles/r01/ab_nt_load.json, ab_ntstore_dma.json).
+__device__ __forceinline__ void st_out(uint32_t *p, uint32_t v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ uint32_t ld_in(const uint32_t *p) { return __builtin_nontemporal_load(p); }
+
+// The 32 words of a lane in a unit, at compile-time offsets from one base
+// pointer (the offsets fold into the instructions' immediate field).
+template <class P, class Off>
+__device__ __forceinline__ void load32(uint32_t (&r)[32], const uint32_t *src, bool valid, Off off)
+{
+#pragma unroll
+    for (int j = 0; j < 32; ++j) r[j] = valid ? ld_in(src + off(j)) : 0u;
+}
+
+// ------------------------------------------------------------------------
+// work distribution
+// ------------------------------------------------------------------------
+// Workgroup b owns the contiguous unit range [b*WAVES*PPW, (b+1)*WAVES*PPW);
+// at step i its waves take consecutive units b*WAVES*PPW + i*WAVES + wave.
+// Workgroups are dispatched in order, so the units in flight chip-wide form a
+// sliding contiguous window of HBM: measured 5.9 TB/s for this access shape
+// vs 5.4 TB/s for a persistent grid-stride loop (profiles/r01/copybw.log).
+// The first unit's global loads are issued before the workgroup prologue
+// (`prologue` = the LDS twiddle-table fill + barrier), so the fill latency
+// hides under the first unit's HBM latency.
+template <int WAVES, class Prologue, class Load, class Process>
+__device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prologue &prologue, Load &load,
+                                           Process &process)
+{
+    uint32_t r[32];
+    uint32_t u = blockIdx.x * (WAVES * ppw) + (threadIdx.x >> 6);
+    if (u < nunits) load(r, u);
+    prologue();   // every wave reaches the barrier inside
+    if (u >= nunits) return;
+    process(r, u);
+#pragma unroll 1
+    for (uint32_t i = 1; i < ppw; ++i) {
+        u += WAVES;
+        if (u >= nunits) break;
+        load(r, u);
+        process(r, u);
+    }
+}
+
+// LDS-DMA prefetch (the launch shape chosen for grids of at most a few
+// workgroup rounds, see launch_for): the next unit's 8 KiB streams HBM -> LDS
+// by global_load_lds_dwordx4 into the wave's transpose buffer -- free from
+// the transpose read until the next unit's first ds_read -- while the current
+// unit's second half and stores run.  No extra VGPRs (a register prefetch
+// would need 32 and cost a wave per SIMD).  In a single workgroup round all
+// waves start in lock step and, without it, load / compute / store in phase
+// (HBM idle while they compute): 65 536 x n=1024 fwd 0.161 -> 0.098 ms.  At
+// many rounds the waves desynchronise by themselves and the DMA's issue cost
+// and extra LDS traffic make it 3 % slower (profiles/r02/ab_small_batch.log).
+// The DMA is inline asm (hipcc would otherwise wait vmcnt(0) -- i.e. for the
+// previous unit's stores too -- before the buffer's ds_reads): its completion
+// is counted by hand.  vmcnt counts loads, stores and LDS-DMA together in
+// issue order (MI355X_MICROARCH.md), and exactly 32 stores follow each DMA,
+// so `s_waitcnt vmcnt(32)` retires precisely the DMA.
+//
+// one 1 KiB piece: lane l's 16 B from gsrc -> LDS byte address lds + 16 l
+__device__ __forceinline__ void dma16(const uint32_t *gsrc, uint32_t lds)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds)
+                 : "memory");
+}
+
+// LDS byte address of a wave-uniform __shared__ pointer
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t *p)
+{
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)p);
+}
+
+// Unit u (2048 consecutive words: one n=2048 poly or two n=1024 polys) ->
+// the wave's buffer in natural order.  `pieces` = 8, or 4 when the unit's
+// second n=1024 poly lies past the batch.
+__device__ __forceinline__ void dma_unit(const uint32_t *unit, uint32_t lds, uint32_t lane, int pieces)
+{
+    const uint32_t *src = unit + 4 * lane;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        if (c < pieces) dma16(src + 256 * c, lds + 1024 * c);
+}
+
+__device__ __forceinline__ void wait_vm(void) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_vm32(void) { asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); }
+__device__ __forceinline__ void wait_lgkm(void) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Work loop with the DMA prefetch: `read(r)` takes the unit from the buffer
+// into registers, `front(r, u)` runs up to and including the last read of the
+// buffer, `back(r, u)` runs the rest and issues exactly 32 stores per lane.
+template <int WAVES, class Prologue, class Read, class Front, class Back>
+__device__ __forceinline__ void chunk_loop_dma(const uint32_t *in, uint32_t npoly, uint32_t nunits, uint32_t ppw,
+                                               uint32_t lds, uint32_t lane, bool half_units, Prologue &prologue,
+                                               Read &read, Front &front, Back &back)
+{
+    auto pieces = [&](uint32_t u) { return (half_units && 2 * u + 1 >= npoly) ? 4 : 8; };
+    uint32_t u = blockIdx.x * (WAVES * ppw) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (u < nunits) dma_unit(in + (size_t)u * 2048, lds, lane, pieces(u));
+    prologue();   // every wave reaches the barrier inside
+    if (u >= nunits) return;
+    wait_vm();
+    uint32_t r[32];
+#pragma unroll 1
+    for (uint32_t i = 0;; ++i) {
+        read(r);
+        front(r, u);
+        wait_lgkm();   // the buffer's last reads are done: it is free
+        const uint32_t un = u + WAVES;
+        const bool more = i + 1 < ppw && un < nunits;
+        if (more) dma_unit(in + (size_t)un * 2048, lds, lane, pieces(un));
+        back(r, u);
+        if (!more) break;
+        u = un;
+        wait_vm32();   // all but the 32 stores issued after the DMA
+    }
+}
+
+// ------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------
+// Workgroup = NTT_WG/64 waves, each with a private 8 KiB transpose buffer;
+// the lane-twiddle table is shared by the workgroup.
+#ifndef NTT_WG
+#define NTT_WG 512   // fwd / inv: 8 waves, 64 + 15.75 KiB LDS -> 2 WG/CU
+#endif
+// poly_mul workgroup per parameter set: n=2048 runs 16 waves (128 + 31.5 KiB
+// LDS, 1 WG/CU, <=128 VGPRs -> 4 waves/SIMD); n=1024 keeps 8 waves at <=256
+// VGPRs (2 waves/SIMD; at 128 VGPRs it spills 60 and loses 37 %),
+// profiles/r01/ab_poly_mul_wg.json
+#ifndef MUL_WG
+#define MUL_WG 512
+#endif
+#ifndef MUL_WG_BIG
+#define MUL_WG_BIG 1024
+#endif
+#ifndef NTT_WAVES_PER_SIMD
+#define NTT_WAVES_PER_SIMD 4
+#endif
+#ifndef MUL_WAVES_PER_SIMD
+#define MUL_WAVES_PER_SIMD 2
+#endif
+#ifndef MUL_WAVES_PER_SIMD_BIG
+#define MUL_WAVES_PER_SIMD_BIG 4
+#endif
+template <int PS> constexpr int mul_wg() { return PSel<PS>::T::LOGN == 11 ? MUL_WG_BIG : MUL_WG; }
+template <int PS> constexpr int mul_occ() { return PSel<PS>::T::LOGN == 11 ? MUL_WAVES_PER_SIMD_BIG : MUL_WAVES_PER_SIMD; }
+constexpr int WG = 256;   // elementwise kernels
+constexpr int NTT_WAVES = NTT_WG / 64;
+constexpr int NTT_LDS_WORDS = NTT_WAVES * XPOSE_WORDS + TW2_WORDS;
+
+// Ordering of the transforms' natural-order boundary (BR = bit-reversed):
+//   forward: natural input; output natural (BR=false) or out[t] = X[brv(t)] (BR=true)
+//   inverse: input natural (BR=false) or in[t] = X[brv(t)] (BR=true); output natural
+// PF: LDS-DMA prefetch work loop (natural order only).
+template <int PS, bool BR, bool PF>
+__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const uint32_t *in, uint32_t *out, uint32_t npoly, uint32_t ppw)
+{
+    static_assert(!(BR && PF), "the prefetch loop serves the natural-order transforms");
+    using P = typename PSel<PS>::T;
+    using LT = Lane<P>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NTT_LDS_WORDS];
+    uint2 *tw2 = reinterpret_cast<uint2 *>(lds + NTT_WAVES * XPOSE_WORDS);
+    auto prologue = [&]() {
+        fill_tw2<PS, false, NTT_WG>(tw2);
+        __syncthreads();
+    };
+    const LT L;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
+    const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
+
+    auto load = [&](uint32_t (&r)[32], uint32_t u) {
+        const uint32_t poly = L.poly(u);
+        load32<P>(r, in + (size_t)poly * P::N + L.brl, LT::BIG || poly < npoly,
+                  [](int j) { return LT::S * j; });   // pass-1 layout: natural lane index
+    };
+    // canonical output: BR=false from the bit-reversed pass-2 registers to
+    // natural order, brv5(j)*S + lane; BR=true from the pass-1 arrangement
+    auto store = [&](uint32_t (&r)[32], uint32_t u) {
+        const uint32_t poly = L.poly(u);
+        if (LT::BIG || poly < npoly) {
+            uint32_t *dst = out + (size_t)poly * P::N + L.brl;
+            if constexpr (BR) dst += LT::BIG ? 32 * L.h : 0u;   // brl + 32 h = l5 + 64 h (p1s_off)
+#pragma unroll
+            for (int j = 0; j < 32; ++j) st_out(dst + (BR ? p1s_off<P>(j) : brv5(j) * LT::S), canon4<P>(r[j]));
+        }
+    };
+    auto front = [&](uint32_t (&r)[32], uint32_t) {
+        fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        lds_p1_to_p2<P>(r, buf, L);
+        if constexpr (BR) {
+            fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+            lds_p2_to_p1<P>(r, buf, L);
+        }
+    };
+    auto back = [&](uint32_t (&r)[32], uint32_t u) {
+        if constexpr (!BR) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        store(r, u);
+    };
+    if constexpr (PF) {
+        const uint32_t *nb = buf + (LT::BIG ? 0u : 1024u * L.h) + L.brl;   // natural image, pass-1 layout
+        auto read = [&](uint32_t (&r)[32]) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) r[j] = nb[LT::S * j];
+        };
+        chunk_loop_dma<NTT_WAVES>(in, npoly, nunits, ppw, lds_addr(buf), L.lane, !LT::BIG, prologue, read, front,
+                                  back);
+    } else {
+        auto process = [&](uint32_t (&r)[32], uint32_t u) {
+            front(r, u);
+            back(r, u);
+        };
+        chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
+    }
+}
+
+template <int PS, bool BR, bool PF>
+__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const uint32_t *in, uint32_t *out, uint32_t npoly, uint32_t ppw)
+{
+    static_assert(!(BR && PF), "the prefetch loop serves the natural-order transforms");
+    using P = typename PSel<PS>::T;
+    using LT = Lane<P>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NTT_LDS_WORDS];
+    uint2 *tw2 = reinterpret_cast<uint2 *>(lds + NTT_WAVES * XPOSE_WORDS);
+    auto prologue = [&]() {
+        fill_tw2<PS, true, NTT_WG>(tw2);
+        __syncthreads();
+    };
+    const LT L;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
+    const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
+
+    // BR=false: natural-order input; pass-2 position 32*Lp + j holds X[brv(pos)]
+    // BR=true:  bit-reversed input read in the pass-1 arrangement, transposed below
+    auto load = [&](uint32_t (&r)[32], uint32_t u) {
+        const uint32_t poly = L.poly(u);
+        const uint32_t *src = in + (size_t)poly * P::N + L.brl;
+        if constexpr (BR) src += LT::BIG ? 32 * L.h : 0u;   // brl + 32 h = l5 + 64 h (p1s_off)
+        load32<P>(r, src, LT::BIG || poly < npoly,
+                  [](int j) { return BR ? p1s_off<P>(j) : brv5(j) * LT::S; });
+    };
+    auto front = [&](uint32_t (&r)[32], uint32_t) {
+        if constexpr (BR) lds_p1_to_p2<P>(r, buf, L);
+        inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        lds_p2_to_p1<P>(r, buf, L);
+    };
+    auto back = [&](uint32_t (&r)[32], uint32_t u) {
+        const uint32_t poly = L.poly(u);
+        uint32_t *dst = out + (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
+        const bool valid = LT::BIG || poly < npoly;
+        auto emit = [&](int j, uint32_t v) {
+            if (valid) st_out(dst + LT::S * j, v);
+        };
+        inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
+    };
+    if constexpr (PF) {
+        const uint32_t *nb = buf + (LT::BIG ? 0u : 1024u * L.h) + L.brl;   // natural image, pass-2 (bit-reversed) layout
+        auto read = [&](uint32_t (&r)[32]) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) r[j] = nb[LT::S * brv5(j)];
+        };
+        chunk_loop_dma<NTT_WAVES>(in, npoly, nunits, ppw, lds_addr(buf), L.lane, !LT::BIG, prologue, read, front,
+                                  back);
+    } else {
+        auto process = [&](uint32_t (&r)[32], uint32_t u) {
+            front(r, u);
+            back(r, u);
+        };
+        chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
+    }
+}
+
+// out[t] = in[brv(t)] per polynomial, any 32-bit words: the pass-1
+// arrangement load -> LDS transpose -> the forward's bit-reversed store
+// mapping (pass-2 register j of lane l holds word 32*Lp + j, stored at
+// brv5(j)*S + l); both sides are 128/256-B runs, no arithmetic.
+template <int PS>
+__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_bitrev(const uint32_t *in, uint32_t *out, uint32_t npoly, uint32_t ppw)
+{
+    using P = typename PSel<PS>::T;
+    using LT = Lane<P>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NTT_WAVES * XPOSE_WORDS];
+    auto prologue = [] {};
+    const LT L;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
+    const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
+    auto load = [&](uint32_t (&r)[32], uint32_t u) {
+        const uint32_t poly = L.poly(u);
+        load32<P>(r, in + (size_t)poly * P::N + L.brl + (LT::BIG ? 32 * L.h : 0u), LT::BIG || poly < npoly,
+                  [](int j) { return p1s_off<P>(j); });
+    };
+    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+        lds_p1_to_p2<P>(r, buf, L);
+        const uint32_t poly = L.poly(u);
+        if (LT::BIG || poly < npoly) {
+            uint32_t *dst = out + (size_t)poly * P::N + L.brl;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) st_out(dst + brv5(j) * LT::S, r[j]);
+        }
+    };
+    chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
+}
+
+// fused c = a*b mod (x^n+1): FWD(a), FWD(b), Montgomery pointwise (the 2^-32
+// is folded into the inverse's final n^-1 scaling), INV -- one HBM read of a
+// and b, one write of c.  BHAT: b is given already transformed (natural-order
+// output of poly_ntt), so only a is transformed -- two transforms of work per
+// product instead of three (poly_mul_ntt).  a, b and c may alias (no
+// __restrict__): every lane loads its words before it stores any.
+template <int PS, bool BHAT>
+__global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
+{
+    using P = typename PSel<PS>::T;
+    using LT = Lane<P>;
+    constexpr int WG_ = mul_wg<PS>();
+    constexpr int WAVES = WG_ / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + 2 * TW2_WORDS];
+    uint2 *ftw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
+    uint2 *itw2 = ftw2 + TW2_WORDS / 2;
+    fill_tw2<PS, false, WG_>(ftw2);
+    fill_tw2<PS, true, WG_>(itw2);
+    __syncthreads();
+    const LT L;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
+
+    const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
+    uint32_t u = blockIdx.x * (WAVES * ppw) + (threadIdx.x >> 6);
+#pragma unroll 1
+    for (uint32_t it = 0; it < ppw; ++it, u += WAVES) {   // dispatch-ordered chunk (see chunk_loop)
+        if (u >= nunits) break;
+        const uint32_t poly = L.poly(u);
+        const bool valid = poly < npoly;
+        const size_t off = (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
+        // a first, then b: the transpose's memory fences keep b's loads below
+        // a's transform, so only ~64 coefficients are live at the peak
+        uint32_t ra[32], rb[32];
+        load32<P>(ra, a + off, valid, [](int j) { return LT::S * j; });
+        fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+        lds_p1_to_p2<P>(ra, buf, L);
+        fwd_pass2<P>(ra, ftw2 + opaque_zero(), L.lane);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            ra[j] = umin(ra[j], ra[j] - P::Q2);
+            // b-hat is in natural order: register j of the pass-2 layout holds
+            // index brv5(j)*S + lane (the forward's store mapping)
+            rb[j] = valid ? ld_in(b + off + LT::S * (BHAT ? brv5(j) : (uint32_t)j)) : 0u;
+        }
+        if constexpr (!BHAT) {
+            fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+            lds_p1_to_p2<P>(rb, buf, L);
+            fwd_pass2<P>(rb, ftw2 + opaque_zero(), L.lane);
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(ra[j], umin(rb[j], rb[j] - P::Q2));   // b-hat < 2q
+        inv_pass2<P>(ra, itw2 + opaque_zero(), L.lane);
+        lds_p2_to_p1<P>(ra, buf, L);
+        uint32_t *pc = c + off;
+        auto emit = [&](int j, uint32_t v) {   // stores interleaved with the last stage (see inv_pass1)
+            if (valid) st_out(pc + LT::S * j, v);
+        };
+        inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
+    }
+}
+
+// c = a.*b mod q over `count` coefficients (count % 4 == 0): Montgomery then
+// Shoup by 2^32 mod q to undo the 2^-32.
+template <int PS>
+__global__ __launch_bounds__(WG) void k_pointwise(const uint4 *a, const uint4 *b, uint4 *c, size_t count4)
+{
+    using P = typename PSel<PS>::T;
+    constexpr uint32_t RP = cshoup(P::R, P::Q);
+    for (size_t i = (size_t)blockIdx.x * WG + threadIdx.x; i < count4; i += (size_t)gridDim.x * WG) {
+        const uint4 x = a[i], y = b[i];
+        uint32_t v[4] = {x.x, x.y, x.z, x.w}, w[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t m = mont_mul<P>(umin(v[k], v[k] - P::Q2), umin(w[k], w[k] - P::Q2));
+            m = shoup_mul<P::Q>(m, P::R, RP);
+            v[k] = umin(m, m - P::Q);
+        }
+        c[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(WG) void k_fill_uniform(uint32_t *x, size_t count, uint32_t q, uint64_t seed, uint64_t first)
+{
+    for (size_t i = (size_t)blockIdx.x * WG + threadIdx.x; i < count; i += (size_t)gridDim.x * WG) {
+        const uint64_t r = splitmix64(seed + (first + i + 1) * 0x9E3779B97F4A7C15ULL);
+        x[i] = (uint32_t)(((r >> 32) * (uint64_t)q) >> 32);
+    }
+}
+
+}  // namespace qntt

@@ -368,8 +368,8 @@ __device__ __forceinline__ void inner_product(uint32_t *xrow, const uint32_t *yr
 }
 
 template <int PS, int RING>
-__global__ __launch_bounds__(NUS_WG, 1) void k_nussbaumer(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
-                                                         uint32_t *c, uint32_t npoly, uint32_t ppw)
+__global__ __launch_bounds__(NUS_WG, 1) void k_nussbaumer(const uint32_t *a, const uint32_t *b, uint32_t *c,
+                                                         uint32_t npoly, uint32_t ppw)
 {
     using P = typename PSel<PS>::T;
     using G = Geo<P::N>;

@@ -13,6 +13,11 @@ Names and argument meaning follow the reference's GPU pipeline
   poly_mul      -- the whole CT-GS poly-mul driver (test_NTT_CT_GS_nega_gpu, :2358)
   poly_pointwise -- pointwise_mult (:1155-1160)
   poly_mul_nussbaumer -- nussbaumer_fft (:167-277), batched, n = 1024 / 2048
+  poly_ntt_bitrev / poly_invntt_bitrev -- the CT-CT ordering: bit-reversed
+                   NTT domain (radix2INTT_gpu0/1/2 on bit-reversed input, :2240-2249)
+
+Every torch wrapper runs on its tensors' device (all operands must share
+one) and, by default, on that device's current stream.
 """
 from __future__ import annotations
 
@@ -75,13 +80,14 @@ def lib():
         L.ntt_get_tables.argtypes = [ctypes.c_int] + [_u32p] * 5
         for nm in ("poly_ntt", "poly_invntt"):
             getattr(L, nm).argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
-        for nm in ("poly_ntt_oop", "poly_invntt_oop", "poly_bitrev_copy"):
+        for nm in ("poly_ntt_oop", "poly_invntt_oop", "poly_bitrev_copy", "poly_ntt_bitrev", "poly_invntt_bitrev"):
             getattr(L, nm).argtypes = [_vp, _vp, _sz, ctypes.c_int, _vp]
         for nm in ("poly_mul", "poly_mul_ntt", "poly_pointwise"):
             getattr(L, nm).argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, _vp]
         L.poly_mul_nussbaumer.argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp]
         L.ntt_fill_uniform.argtypes = [_vp, _sz, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp]
         L.ntt_last_hip_error.restype = ctypes.c_int
+        L.ntt_set_prefetch.argtypes = [ctypes.c_int]
         L.ntt_strerror.restype = ctypes.c_char_p
         L.ntt_strerror.argtypes = [ctypes.c_int]
         L.ntt_build_info.argtypes = [ctypes.c_char_p, _sz]
@@ -121,9 +127,24 @@ def tables(param_set) -> dict:
 
 
 def build_info() -> str:
-    buf = ctypes.create_string_buffer(512)
-    lib().ntt_build_info(buf, 512)
+    buf = ctypes.create_string_buffer(1024)
+    lib().ntt_build_info(buf, 1024)
     return buf.value.decode()
+
+
+def set_prefetch(policy: int) -> int:
+    """Work loop of the transforms: -1 automatic, 0 never, 1 always prefetch
+    (ntt_set_prefetch); returns the previous policy."""
+    rc = lib().ntt_set_prefetch(int(policy))
+    if rc < -1:
+        raise NTTError(rc, "ntt_set_prefetch")
+    return rc
+
+
+def build_hash() -> str:
+    """Hash of the library sources the loaded .so was built from ("src=" field)."""
+    info = build_info()
+    return info.rsplit("src=", 1)[1].strip() if "src=" in info else "unknown"
 
 
 # ---------------------------------------------------------------- raw API
@@ -148,10 +169,23 @@ def _torch():
     return torch
 
 
-def _stream(stream):
+def _device_of(*tensors):
+    """The one device all operands live on (ValueError otherwise)."""
+    dev = None
+    for t in tensors:
+        if not getattr(t, "is_cuda", False):
+            raise ValueError("ntt_amd operates on device tensors only (no CPU fallback)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"operands on different devices: {dev} and {t.device}")
+    return dev
+
+
+def _stream(stream, device=None):
     torch = _torch()
     if stream is None:
-        return torch.cuda.current_stream().cuda_stream
+        return torch.cuda.current_stream(device).cuda_stream
     return stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
 
 
@@ -168,69 +202,86 @@ def _batch(t, n: int) -> int:
     return t.numel() // n
 
 
+def _run(where: str, tensors, stream, call):
+    """Check the operands, make their device current and call `call(stream)`."""
+    dev = _device_of(*tensors)
+    torch = _torch()
+    with torch.cuda.device(dev):
+        _check(call(_stream(stream, dev)), where)
+
+
+def _same_batch(n: int, first, *others) -> int:
+    b = _batch(first, n)
+    for o in others:
+        if _batch(o, n) != b:
+            raise ValueError("batch mismatch")
+    return b
+
+
 def poly_ntt(t, param_set, stream=None):
     """In-place forward negacyclic NTT of a [batch, n] device tensor."""
     n = param_info(param_set)["n"]
-    _check(lib().poly_ntt(t.data_ptr(), None, _batch(t, n), _ps(param_set), _stream(stream)), "poly_ntt")
+    b = _batch(t, n)
+    _run("poly_ntt", (t,), stream, lambda s: lib().poly_ntt(t.data_ptr(), None, b, _ps(param_set), s))
     return t
 
 
 def poly_invntt(t, param_set, stream=None):
     """In-place inverse negacyclic NTT (includes n^-1 and psi^-i)."""
     n = param_info(param_set)["n"]
-    _check(lib().poly_invntt(t.data_ptr(), None, _batch(t, n), _ps(param_set), _stream(stream)), "poly_invntt")
+    b = _batch(t, n)
+    _run("poly_invntt", (t,), stream, lambda s: lib().poly_invntt(t.data_ptr(), None, b, _ps(param_set), s))
     return t
 
 
-def poly_ntt_oop(out, inp, param_set, stream=None):
+def _oop(name, out, inp, param_set, stream):
     n = param_info(param_set)["n"]
-    b = _batch(inp, n)
-    if _batch(out, n) != b:
-        raise ValueError("out/in batch mismatch")
-    _check(lib().poly_ntt_oop(out.data_ptr(), inp.data_ptr(), b, _ps(param_set), _stream(stream)), "poly_ntt_oop")
+    b = _same_batch(n, inp, out)
+    fn = getattr(lib(), name)
+    _run(name, (out, inp), stream, lambda s: fn(out.data_ptr(), inp.data_ptr(), b, _ps(param_set), s))
     return out
+
+
+def poly_ntt_oop(out, inp, param_set, stream=None):
+    return _oop("poly_ntt_oop", out, inp, param_set, stream)
 
 
 def poly_invntt_oop(out, inp, param_set, stream=None):
-    n = param_info(param_set)["n"]
-    b = _batch(inp, n)
-    if _batch(out, n) != b:
-        raise ValueError("out/in batch mismatch")
-    _check(lib().poly_invntt_oop(out.data_ptr(), inp.data_ptr(), b, _ps(param_set), _stream(stream)),
-           "poly_invntt_oop")
-    return out
+    return _oop("poly_invntt_oop", out, inp, param_set, stream)
+
+
+def poly_ntt_bitrev(out, inp, param_set, stream=None):
+    """Forward NTT with bit-reversed output order: out[b, t] = X[b, brv(t)]."""
+    return _oop("poly_ntt_bitrev", out, inp, param_set, stream)
+
+
+def poly_invntt_bitrev(out, inp, param_set, stream=None):
+    """Inverse NTT of a bit-reversed-order input (inp[b, t] = X[b, brv(t)])."""
+    return _oop("poly_invntt_bitrev", out, inp, param_set, stream)
 
 
 def poly_bitrev_copy(out, inp, param_set, stream=None):
     """out[b, t] = inp[b, brv(t)] (bit_reverse_copy_tbl_gpu); out may be inp."""
+    return _oop("poly_bitrev_copy", out, inp, param_set, stream)
+
+
+def _mul(name, c, a, b, param_set, stream, *extra):
     n = param_info(param_set)["n"]
-    b = _batch(inp, n)
-    if _batch(out, n) != b:
-        raise ValueError("out/in batch mismatch")
-    _check(lib().poly_bitrev_copy(out.data_ptr(), inp.data_ptr(), b, _ps(param_set), _stream(stream)),
-           "poly_bitrev_copy")
-    return out
+    nb = _same_batch(n, a, b, c)
+    fn = getattr(lib(), name)
+    _run(name, (c, a, b), stream,
+         lambda s: fn(c.data_ptr(), a.data_ptr(), b.data_ptr(), nb, _ps(param_set), *extra, s))
+    return c
 
 
 def poly_mul(c, a, b, param_set, stream=None):
     """c = a*b mod (x^n + 1, q), fused single launch."""
-    n = param_info(param_set)["n"]
-    nb = _batch(a, n)
-    if _batch(b, n) != nb or _batch(c, n) != nb:
-        raise ValueError("batch mismatch")
-    _check(lib().poly_mul(c.data_ptr(), a.data_ptr(), b.data_ptr(), nb, _ps(param_set), _stream(stream)), "poly_mul")
-    return c
+    return _mul("poly_mul", c, a, b, param_set, stream)
 
 
 def poly_mul_ntt(c, a, bhat, param_set, stream=None):
     """c = a*b mod (x^n + 1, q) with bhat = poly_ntt(b) given (NTT domain)."""
-    n = param_info(param_set)["n"]
-    nb = _batch(a, n)
-    if _batch(bhat, n) != nb or _batch(c, n) != nb:
-        raise ValueError("batch mismatch")
-    _check(lib().poly_mul_ntt(c.data_ptr(), a.data_ptr(), bhat.data_ptr(), nb, _ps(param_set), _stream(stream)),
-           "poly_mul_ntt")
-    return c
+    return _mul("poly_mul_ntt", c, a, bhat, param_set, stream)
 
 
 def poly_mul_nussbaumer(c, a, b, param_set, ring="q", stream=None):
@@ -238,31 +289,20 @@ def poly_mul_nussbaumer(c, a, b, param_set, ring="q", stream=None):
 
     ring "q": mod param_set's q (equals poly_mul); ring "m32": mod 2^32 - 1,
     the reference's ring.  Buffers must be 16-byte aligned."""
-    n = param_info(param_set)["n"]
-    nb = _batch(a, n)
-    if _batch(b, n) != nb or _batch(c, n) != nb:
-        raise ValueError("batch mismatch")
     r = RINGS[ring] if isinstance(ring, str) else int(ring)
-    _check(lib().poly_mul_nussbaumer(c.data_ptr(), a.data_ptr(), b.data_ptr(), nb, _ps(param_set), r,
-                                     _stream(stream)), "poly_mul_nussbaumer")
-    return c
+    return _mul("poly_mul_nussbaumer", c, a, b, param_set, stream, r)
 
 
 def poly_pointwise(c, a, b, param_set, stream=None):
-    n = param_info(param_set)["n"]
-    nb = _batch(a, n)
-    if _batch(b, n) != nb or _batch(c, n) != nb:
-        raise ValueError("batch mismatch")
-    _check(lib().poly_pointwise(c.data_ptr(), a.data_ptr(), b.data_ptr(), nb, _ps(param_set), _stream(stream)),
-           "poly_pointwise")
-    return c
+    return _mul("poly_pointwise", c, a, b, param_set, stream)
 
 
 def fill_uniform(t, param_set, seed: int, first_poly: int = 0, stream=None):
     """Device-side counter-based uniform coefficients in [0, q)."""
     n = param_info(param_set)["n"]
-    _check(lib().ntt_fill_uniform(t.data_ptr(), _batch(t, n), _ps(param_set), seed & (2**64 - 1), first_poly,
-                                  _stream(stream)), "ntt_fill_uniform")
+    b = _batch(t, n)
+    _run("ntt_fill_uniform", (t,), stream,
+         lambda s: lib().ntt_fill_uniform(t.data_ptr(), b, _ps(param_set), seed & (2**64 - 1), first_poly, s))
     return t
 
 

@@ -1,0 +1,169 @@
+// ntt_diag.hip -- tools-only library (lib/libqtesla_ntt_diag.so, `make tools`)
+// for bottleneck attribution of the transform kernels: the production kernels
+// of csrc/ntt_device.hpp next to variants that keep one side of them only.
+// Never linked into libqtesla_ntt.so; used by tools/variants.py.
+//
+//   variant 0  full kernel (k_ntt_fwd / k_ntt_inv, natural order, no prefetch)
+//   variant 1  global load + store only (same addresses, grid and work loop)
+//   variant 2  arithmetic + LDS transposes only (no global memory)
+//   variant 3  load + LDS transpose(s) + store (no arithmetic)
+//   op 2       plain copies of n=2048 polys, one per wave: dword (variant 0)
+//              or dwordx4 (variant 1) accesses
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+
+#include "../../include/qtesla_ntt.h"
+#include "../csrc/dev_tables.hpp"
+#include "../csrc/ntt_device.hpp"
+
+namespace qntt {
+namespace {
+
+// keeps a value live without storing it
+__device__ __forceinline__ void sink(uint32_t v) { asm volatile("" ::"v"(v)); }
+
+template <int PS, bool INV, int V>
+__global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_variant(const uint32_t *in, uint32_t *out, uint32_t npoly, uint32_t ppw)
+{
+    using P = typename PSel<PS>::T;
+    using LT = Lane<P>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NTT_LDS_WORDS];
+    uint2 *tw2 = reinterpret_cast<uint2 *>(lds + NTT_WAVES * XPOSE_WORDS);
+    auto prologue = [&]() {
+        fill_tw2<PS, INV, NTT_WG>(tw2);
+        __syncthreads();
+    };
+    const LT L;
+    uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
+    const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
+    auto load = [&](uint32_t (&r)[32], uint32_t u) {
+        const uint32_t poly = L.poly(u);
+        if constexpr (V == 2) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) r[j] = L.lane * (j + u);
+        } else {
+            load32<P>(r, in + (size_t)poly * P::N + L.brl, LT::BIG || poly < npoly,
+                      [](int j) { return INV ? brv5(j) * LT::S : LT::S * j; });
+        }
+    };
+    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+        const uint32_t poly = L.poly(u);
+        if constexpr (!INV) {
+            if constexpr (V == 2) fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+            if constexpr (V != 1) lds_p1_to_p2<P>(r, buf, L);
+            if constexpr (V == 2) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        } else {
+            if constexpr (V == 2) inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+            if constexpr (V != 1) lds_p2_to_p1<P>(r, buf, L);
+            if constexpr (V == 2) inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        }
+        if (LT::BIG || poly < npoly) {
+            uint32_t *dst = out + (size_t)poly * P::N + L.brl;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                if constexpr (V == 2) sink(r[j]);
+                else st_out(dst + (INV ? LT::S * j : brv5(j) * LT::S), r[j]);
+            }
+        }
+    };
+    chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
+}
+
+template <int W>
+__global__ __launch_bounds__(512) void k_copy_diag(const uint32_t *in, uint32_t *out, uint32_t npoly)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * 8;
+    for (uint32_t u = blockIdx.x * 8 + (threadIdx.x >> 6); u < npoly; u += nw) {
+        if constexpr (W == 4) {
+            const uint4 *s4 = reinterpret_cast<const uint4 *>(in + (size_t)u * 2048) + lane;
+            uint4 *d4 = reinterpret_cast<uint4 *>(out + (size_t)u * 2048) + lane;
+            uint4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = s4[64 * j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d4[64 * j] = v[j];
+        } else {
+            const uint32_t *s1 = in + (size_t)u * 2048 + lane;
+            uint32_t *d1 = out + (size_t)u * 2048 + lane;
+            uint32_t v[32];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) v[j] = s1[64 * j];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) d1[64 * j] = v[j];
+        }
+    }
+}
+
+std::once_flag g_once;
+hipError_t g_upload = hipSuccess;
+int g_cus = 256;
+
+template <int PS>
+int launch(int op, int variant, uint32_t *out, const uint32_t *in, uint32_t nb, hipStream_t s)
+{
+    using P = typename PSel<PS>::T;
+    const uint32_t units = (nb + Lane<P>::UPW - 1) / Lane<P>::UPW;
+    uint32_t ppw = units / (NTT_WAVES * 2 * g_cus);
+    ppw = ppw < 1 ? 1 : (ppw > 16 ? 16 : ppw);
+    const dim3 g((units + NTT_WAVES * ppw - 1) / (NTT_WAVES * ppw)), b(NTT_WG);
+#define QNTT_V(INV, V) hipLaunchKernelGGL((k_variant<PS, INV, V>), g, b, 0, s, in, out, nb, ppw)
+    switch (op * 16 + variant) {
+    case 0: hipLaunchKernelGGL((k_ntt_fwd<PS, false, false>), g, b, 0, s, in, out, nb, ppw); break;
+    case 1: QNTT_V(false, 1); break;
+    case 2: QNTT_V(false, 2); break;
+    case 3: QNTT_V(false, 3); break;
+    case 16: hipLaunchKernelGGL((k_ntt_inv<PS, false, false>), g, b, 0, s, in, out, nb, ppw); break;
+    case 17: QNTT_V(true, 1); break;
+    case 18: QNTT_V(true, 2); break;
+    case 19: QNTT_V(true, 3); break;
+    default: return NTT_ERR_PARAM;
+    }
+#undef QNTT_V
+    return hipGetLastError() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+}
+
+}  // namespace
+}  // namespace qntt
+
+using namespace qntt;
+
+extern "C" int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uint32_t *d_in, size_t batch, int ps,
+                                 void *stream)
+{
+    const ParamSet *p = param_set(ps);
+    if (!p) return NTT_ERR_PARAM;
+    if (batch == 0) return NTT_OK;
+    if (!d_in || !d_out) return NTT_ERR_NULL;
+    if ((((uintptr_t)d_in) | ((uintptr_t)d_out)) & 15u) return NTT_ERR_ALIGN;
+    if (batch > 0x7FFFFFFF) return NTT_ERR_SIZE;
+    const size_t bytes = batch * p->n * 4;
+    const uintptr_t a = (uintptr_t)d_in, b = (uintptr_t)d_out;
+    if (a != b && a < b + bytes && b < a + bytes) return NTT_ERR_ALIAS;
+    std::call_once(g_once, [] {
+        Tables tabs[3];
+        for (int i = 0; i < 3; i++) make_tables(*param_set(i), tabs[i]);
+        g_upload = upload_device_tables(tabs);
+        int dev = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+            g_cus = prop.multiProcessorCount;
+    });
+    if (g_upload != hipSuccess) return NTT_ERR_HIP;
+    hipStream_t s = (hipStream_t)stream;
+    if (op == 2) {   // copies of n = 2048 polys, 2 workgroups of 8 waves per CU
+        if (p->n != 2048) return NTT_ERR_PARAM;
+        const dim3 g2((uint32_t)g_cus * 2);
+        if (variant == 0) hipLaunchKernelGGL((k_copy_diag<1>), g2, dim3(512), 0, s, d_in, d_out, (uint32_t)batch);
+        else hipLaunchKernelGGL((k_copy_diag<4>), g2, dim3(512), 0, s, d_in, d_out, (uint32_t)batch);
+        return hipGetLastError() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    }
+    if (op != 0 && op != 1) return NTT_ERR_PARAM;
+    switch (ps) {
+    case 0: return launch<0>(op, variant, d_out, d_in, (uint32_t)batch, s);
+    case 1: return launch<1>(op, variant, d_out, d_in, (uint32_t)batch, s);
+    default: return launch<2>(op, variant, d_out, d_in, (uint32_t)batch, s);
+    }
+}

@@ -33,6 +33,11 @@ def test_error_codes_before_any_gpu_work(ntt):
     assert L.poly_pointwise(fake + 4, fake, fake + 0x100000, 1, 2, None) == ntt.NTT_ERR_ALIGN
     assert L.ntt_fill_uniform(None, 1, 1, 0, 0, None) == ntt.NTT_ERR_NULL
     assert L.poly_ntt(fake, None, 1 << 31, 2, None) == ntt.NTT_ERR_SIZE
+    assert L.poly_ntt_bitrev(fake, fake + 4, 2, 0, None) == ntt.NTT_ERR_ALIAS
+    assert L.poly_invntt_bitrev(None, fake, 1, 2, None) == ntt.NTT_ERR_NULL
+    assert L.ntt_set_prefetch(2) == ntt.NTT_ERR_PARAM
+    old = ntt.set_prefetch(0)
+    assert ntt.set_prefetch(old) == 0
     for code in (0, -1, -2, -3, -4, -5, -6):
         assert L.ntt_strerror(code)
     with pytest.raises(KeyError):
@@ -44,6 +49,8 @@ def test_param_info(ntt):
     assert ntt.param_info("p-I")["q"] == 343576577 and ntt.param_info("p-I")["n"] == 1024
     assert ntt.param_info("p-III")["q"] == 856145921 and ntt.param_info("p-III")["n"] == 2048
     assert "gfx950" in ntt.build_info()
+    h = ntt.build_hash()
+    assert len(h) == 16 and all(c in "0123456789abcdef" for c in h), h
 
 
 def test_cpu_tensor_rejected(ntt):

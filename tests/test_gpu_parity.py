@@ -42,9 +42,17 @@ def test_golden_vectors(ntt, oracle, dev, ps):
     assert np.array_equal(_u32(ntt, t)[0], g["pattern"])
 
 
+@pytest.fixture(params=[-1, 0, 1], ids=["loop-auto", "loop-plain", "loop-prefetch"])
+def prefetch(request, ntt):
+    """Run the test under each work-loop policy of the transforms (ntt_set_prefetch)."""
+    old = ntt.set_prefetch(request.param)
+    yield request.param
+    ntt.set_prefetch(old)
+
+
 @pytest.mark.parametrize("ps", PARAM_SETS)
-@pytest.mark.parametrize("batch", [1, 2, 3, 64, 257])
-def test_fwd_inv_random(ntt, oracle, dev, ps, batch):
+@pytest.mark.parametrize("batch", [1, 2, 3, 64, 257, 8195])
+def test_fwd_inv_random(ntt, oracle, dev, ps, batch, prefetch):
     x = oracle.fill_uniform(batch, ps, 0xC0FFEE + batch, 0)
     t = _dev(ntt, x, dev)
     ntt.poly_ntt(t, ps)
@@ -57,6 +65,36 @@ def test_fwd_inv_random(ntt, oracle, dev, ps, batch):
     t = _dev(ntt, Y, dev)
     ntt.poly_invntt(t, ps)
     assert np.array_equal(_u32(ntt, t), oracle.poly_invntt(Y, ps))
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+@pytest.mark.parametrize("batch", [1, 3, 130])
+def test_bitrev_order_transforms(ntt, oracle, dev, ps, batch):
+    """poly_ntt_bitrev / poly_invntt_bitrev: the NTT domain in bit-reversed order,
+    as the reference's CT-CT pipeline keeps it (bit_reverse_copy_tbl_gpu +
+    radix2INTT_gpu0/1/2 on bit-reversed input, NTT.cu:2239-2249)."""
+    br = ntt.tables(ps)["bitrev_tbl"]
+    x = oracle.fill_uniform(batch, ps, 0xB17 + batch, 0)
+    X = oracle.poly_ntt(x, ps)
+    tx = _dev(ntt, x, dev)
+    o = torch.empty_like(tx)
+    ntt.poly_ntt_bitrev(o, tx, ps)
+    assert np.array_equal(_u32(ntt, o), X[:, br])
+    assert np.array_equal(_u32(ntt, tx), x)            # out of place keeps the input
+    ntt.poly_invntt_bitrev(tx, o, ps)
+    assert np.array_equal(_u32(ntt, tx), x)
+    # inverse of an arbitrary bit-reversed-order vector vs the oracle's CT-CT inverse
+    Ybr = oracle.fill_uniform(batch, ps, 0xB18 + batch, 0)
+    want = oracle.poly_invntt_ct(oracle.bit_reverse_copy(Ybr, ps), ps)
+    assert np.array_equal(want, oracle.poly_invntt(Ybr[:, br], ps))
+    t = _dev(ntt, Ybr, dev)
+    ntt.poly_invntt_bitrev(t, t, ps)                     # in place
+    assert np.array_equal(_u32(ntt, t), want)
+    # the CT-CT composition: bitrev copy then the bit-reversed inverse == poly_invntt
+    t = _dev(ntt, X, dev)
+    ntt.poly_bitrev_copy(t, t, ps)
+    ntt.poly_invntt_bitrev(t, t, ps)
+    assert np.array_equal(_u32(ntt, t), x)
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
@@ -167,6 +205,26 @@ def test_batch_zero_and_errors(ntt, dev):
         ntt.poly_ntt(t, 9)
 
 
+def test_device_checks(ntt, dev):
+    """Operands on different devices are rejected; a tensor on a non-current
+    device runs on its own device and stream."""
+    n = 2048
+    a = torch.zeros(n, dtype=torch.int32, device=dev)
+    with pytest.raises(ValueError):
+        ntt.poly_mul(a, a, torch.zeros(n, dtype=torch.int32), "p-III")
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU: the non-current-device case needs two")
+    other = torch.device("cuda", 1)
+    b = torch.ones(n, dtype=torch.int32, device=other)
+    with pytest.raises(ValueError):
+        ntt.poly_mul(a, a, b, "p-III")
+    with torch.cuda.device(0):
+        ntt.poly_ntt(b, "p-III")
+        ntt.poly_invntt(b, "p-III")
+    torch.cuda.synchronize(other)
+    assert torch.equal(b.cpu(), torch.ones(n, dtype=torch.int32))
+
+
 def test_nondefault_stream(ntt, oracle, dev):
     ps = "p-III"
     x = oracle.fill_uniform(50, ps, 5, 0)
@@ -180,7 +238,7 @@ def test_nondefault_stream(ntt, oracle, dev):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("ps,batch", [("p-III", 1 << 20), ("p-I", 65536), ("ref", 65536)])
+@pytest.mark.parametrize("ps,batch", [("p-III", 1 << 20), ("p-I", 65536), ("ref", 65536), ("p-III", 300001)])
 def test_full_batch_properties(ntt, oracle, dev, ps, batch):
     """BASELINE sizes: round trip on the whole batch on device + sampled polys vs oracle."""
     n = ntt.param_info(ps)["n"]

@@ -2,7 +2,8 @@
 """Bottleneck attribution for the transform kernels (diagnostic, not the bench).
 
 Times, interleaved in one process (guide rule 24), the production kernel and
-its diagnostic variants through ntt_debug_variant (csrc/ntt_internal.h):
+its diagnostic variants through ntt_debug_variant of the tools-only library
+lib/libqtesla_ntt_diag.so (ntt-gpu-qtesla_amd/tools/ntt_diag.hip, `make tools`):
   full | mem (global load+store only) | alu (no global memory) | lds (load+LDS transpose+store)
 plus torch's device copy of the same bytes as an achievable-bandwidth yardstick.
 """
@@ -25,7 +26,8 @@ def main():
     args = ap.parse_args()
     import torch
     import ntt_amd
-    L = ntt_amd.lib()
+    ntt_amd.lib()   # binds the HIP runtime torch loaded (see ntt_amd.lib)
+    L = ctypes.CDLL(os.path.join(ROOT, "ntt-gpu-qtesla_amd", "lib", "libqtesla_ntt_diag.so"))
     L.ntt_debug_variant.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                     ctypes.c_int, ctypes.c_void_p]
     ps = ntt_amd.PARAM_SETS[args.param]
