@@ -184,15 +184,6 @@ void ntt_host_free(void *p);
 int ntt_last_hip_error(void);
 const char *ntt_strerror(int code);
 
-/* Tuning: work loop of the transforms (poly_ntt / poly_invntt and their _oop
- * forms).  -1 (default) = automatic: LDS-DMA prefetch of the next polynomial
- * for launches of at most two workgroup rounds (small batches, where all
- * waves would otherwise load, compute and store in phase), the plain loop
- * above that; 0 = never; 1 = always.  Results are identical either way.
- * Process-wide; the initial value may be set by the environment variable
- * QTESLA_NTT_PREFETCH=0|1.  Returns the previous policy, or NTT_ERR_PARAM. */
-int ntt_set_prefetch(int policy);
-
 /* Library / kernel description for reports, ending in "src=<16 hex>" (a hash
  * of the library sources): writes at most len bytes, returns the length. */
 int ntt_build_info(char *buf, size_t len);

@@ -160,6 +160,16 @@ struct Lane {
     }
     // index of this lane's polynomial in wave unit u
     __device__ __forceinline__ uint32_t poly(uint32_t u) const { return u * UPW + (BIG ? 0u : h); }
+    // the polynomial this lane loads from: its own, or for the second half of
+    // the batch's last n=1024 unit when the batch is odd, the unit's first
+    // (valid) one -- loads stay unconditional (no exec masking and no selects
+    // per load, which cost ~900 v_mov_b64 per unit in the plain loop); the
+    // results of such lanes are never stored
+    __device__ __forceinline__ uint32_t load_poly(uint32_t u, uint32_t npoly) const
+    {
+        const uint32_t p = poly(u);
+        return (BIG || p < npoly) ? p : u * UPW;
+    }
 };
 
 // pos>>5 of register j in the pass-1 layout (n=2048: after the bit-5 swap)
@@ -418,11 +428,11 @@ __device__ __forceinline__ uint32_t ld_in(const uint32_t *p) { return __builtin_
 
 // The 32 words of a lane in a unit, at compile-time offsets from one base
 // pointer (the offsets fold into the instructions' immediate field).
-template <class P, class Off>
-__device__ __forceinline__ void load32(uint32_t (&r)[32], const uint32_t *src, bool valid, Off off)
+template <class Off>
+__device__ __forceinline__ void load32(uint32_t (&r)[32], const uint32_t *src, Off off)
 {
 #pragma unroll
-    for (int j = 0; j < 32; ++j) r[j] = valid ? ld_in(src + off(j)) : 0u;
+    for (int j = 0; j < 32; ++j) r[j] = ld_in(src + off(j));
 }
 
 // ------------------------------------------------------------------------
@@ -452,83 +462,6 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
         if (u >= nunits) break;
         load(r, u);
         process(r, u);
-    }
-}
-
-// LDS-DMA prefetch (the launch shape chosen for grids of at most a few
-// workgroup rounds, see launch_for): the next unit's 8 KiB streams HBM -> LDS
-// by global_load_lds_dwordx4 into the wave's transpose buffer -- free from
-// the transpose read until the next unit's first ds_read -- while the current
-// unit's second half and stores run.  No extra VGPRs (a register prefetch
-// would need 32 and cost a wave per SIMD).  In a single workgroup round all
-// waves start in lock step and, without it, load / compute / store in phase
-// (HBM idle while they compute): 65 536 x n=1024 fwd 0.161 -> 0.098 ms.  At
-// many rounds the waves desynchronise by themselves and the DMA's issue cost
-// and extra LDS traffic make it 3 % slower (profiles/r02/ab_small_batch.log).
-// The DMA is inline asm (hipcc would otherwise wait vmcnt(0) -- i.e. for the
-// previous unit's stores too -- before the buffer's ds_reads): its completion
-// is counted by hand.  vmcnt counts loads, stores and LDS-DMA together in
-// issue order (MI355X_MICROARCH.md), and exactly 32 stores follow each DMA,
-// so `s_waitcnt vmcnt(32)` retires precisely the DMA.
-//
-// one 1 KiB piece: lane l's 16 B from gsrc -> LDS byte address lds + 16 l
-__device__ __forceinline__ void dma16(const uint32_t *gsrc, uint32_t lds)
-{
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds)
-                 : "memory");
-}
-
-// LDS byte address of a wave-uniform __shared__ pointer
-__device__ __forceinline__ uint32_t lds_addr(const uint32_t *p)
-{
-    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)p);
-}
-
-// Unit u (2048 consecutive words: one n=2048 poly or two n=1024 polys) ->
-// the wave's buffer in natural order.  `pieces` = 8, or 4 when the unit's
-// second n=1024 poly lies past the batch.
-__device__ __forceinline__ void dma_unit(const uint32_t *unit, uint32_t lds, uint32_t lane, int pieces)
-{
-    const uint32_t *src = unit + 4 * lane;
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-        if (c < pieces) dma16(src + 256 * c, lds + 1024 * c);
-}
-
-__device__ __forceinline__ void wait_vm(void) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void wait_vm32(void) { asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); }
-__device__ __forceinline__ void wait_lgkm(void) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-// Work loop with the DMA prefetch: `read(r)` takes the unit from the buffer
-// into registers, `front(r, u)` runs up to and including the last read of the
-// buffer, `back(r, u)` runs the rest and issues exactly 32 stores per lane.
-template <int WAVES, class Prologue, class Read, class Front, class Back>
-__device__ __forceinline__ void chunk_loop_dma(const uint32_t *in, uint32_t npoly, uint32_t nunits, uint32_t ppw,
-                                               uint32_t lds, uint32_t lane, bool half_units, Prologue &prologue,
-                                               Read &read, Front &front, Back &back)
-{
-    auto pieces = [&](uint32_t u) { return (half_units && 2 * u + 1 >= npoly) ? 4 : 8; };
-    uint32_t u = blockIdx.x * (WAVES * ppw) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (u < nunits) dma_unit(in + (size_t)u * 2048, lds, lane, pieces(u));
-    prologue();   // every wave reaches the barrier inside
-    if (u >= nunits) return;
-    wait_vm();
-    uint32_t r[32];
-#pragma unroll 1
-    for (uint32_t i = 0;; ++i) {
-        read(r);
-        front(r, u);
-        wait_lgkm();   // the buffer's last reads are done: it is free
-        const uint32_t un = u + WAVES;
-        const bool more = i + 1 < ppw && un < nunits;
-        if (more) dma_unit(in + (size_t)un * 2048, lds, lane, pieces(un));
-        back(r, u);
-        if (!more) break;
-        u = un;
-        wait_vm32();   // all but the 32 stores issued after the DMA
     }
 }
 
@@ -568,11 +501,9 @@ constexpr int NTT_LDS_WORDS = NTT_WAVES * XPOSE_WORDS + TW2_WORDS;
 // Ordering of the transforms' natural-order boundary (BR = bit-reversed):
 //   forward: natural input; output natural (BR=false) or out[t] = X[brv(t)] (BR=true)
 //   inverse: input natural (BR=false) or in[t] = X[brv(t)] (BR=true); output natural
-// PF: LDS-DMA prefetch work loop (natural order only).
-template <int PS, bool BR, bool PF>
+template <int PS, bool BR>
 __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const uint32_t *in, uint32_t *out, uint32_t npoly, uint32_t ppw)
 {
-    static_assert(!(BR && PF), "the prefetch loop serves the natural-order transforms");
     using P = typename PSel<PS>::T;
     using LT = Lane<P>;
     __shared__ __attribute__((aligned(16))) uint32_t lds[NTT_LDS_WORDS];
@@ -585,10 +516,8 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
 
-    auto load = [&](uint32_t (&r)[32], uint32_t u) {
-        const uint32_t poly = L.poly(u);
-        load32<P>(r, in + (size_t)poly * P::N + L.brl, LT::BIG || poly < npoly,
-                  [](int j) { return LT::S * j; });   // pass-1 layout: natural lane index
+    auto load = [&](uint32_t (&r)[32], uint32_t u) {   // pass-1 layout: natural lane index
+        load32(r, in + (size_t)L.load_poly(u, npoly) * P::N + L.brl, [](int j) { return LT::S * j; });
     };
     // canonical output: BR=false from the bit-reversed pass-2 registers to
     // natural order, brv5(j)*S + lane; BR=true from the pass-1 arrangement
@@ -613,27 +542,16 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
         if constexpr (!BR) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
         store(r, u);
     };
-    if constexpr (PF) {
-        const uint32_t *nb = buf + (LT::BIG ? 0u : 1024u * L.h) + L.brl;   // natural image, pass-1 layout
-        auto read = [&](uint32_t (&r)[32]) {
-#pragma unroll
-            for (int j = 0; j < 32; ++j) r[j] = nb[LT::S * j];
-        };
-        chunk_loop_dma<NTT_WAVES>(in, npoly, nunits, ppw, lds_addr(buf), L.lane, !LT::BIG, prologue, read, front,
-                                  back);
-    } else {
-        auto process = [&](uint32_t (&r)[32], uint32_t u) {
-            front(r, u);
-            back(r, u);
-        };
-        chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
-    }
+    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+        front(r, u);
+        back(r, u);
+    };
+    chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
 }
 
-template <int PS, bool BR, bool PF>
+template <int PS, bool BR>
 __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const uint32_t *in, uint32_t *out, uint32_t npoly, uint32_t ppw)
 {
-    static_assert(!(BR && PF), "the prefetch loop serves the natural-order transforms");
     using P = typename PSel<PS>::T;
     using LT = Lane<P>;
     __shared__ __attribute__((aligned(16))) uint32_t lds[NTT_LDS_WORDS];
@@ -649,11 +567,9 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
     // BR=false: natural-order input; pass-2 position 32*Lp + j holds X[brv(pos)]
     // BR=true:  bit-reversed input read in the pass-1 arrangement, transposed below
     auto load = [&](uint32_t (&r)[32], uint32_t u) {
-        const uint32_t poly = L.poly(u);
-        const uint32_t *src = in + (size_t)poly * P::N + L.brl;
+        const uint32_t *src = in + (size_t)L.load_poly(u, npoly) * P::N + L.brl;
         if constexpr (BR) src += LT::BIG ? 32 * L.h : 0u;   // brl + 32 h = l5 + 64 h (p1s_off)
-        load32<P>(r, src, LT::BIG || poly < npoly,
-                  [](int j) { return BR ? p1s_off<P>(j) : brv5(j) * LT::S; });
+        load32(r, src, [](int j) { return BR ? p1s_off<P>(j) : brv5(j) * LT::S; });
     };
     auto front = [&](uint32_t (&r)[32], uint32_t) {
         if constexpr (BR) lds_p1_to_p2<P>(r, buf, L);
@@ -669,21 +585,11 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
         };
         inv_pass1<PS, P, P::NINV, P::C1>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
     };
-    if constexpr (PF) {
-        const uint32_t *nb = buf + (LT::BIG ? 0u : 1024u * L.h) + L.brl;   // natural image, pass-2 (bit-reversed) layout
-        auto read = [&](uint32_t (&r)[32]) {
-#pragma unroll
-            for (int j = 0; j < 32; ++j) r[j] = nb[LT::S * brv5(j)];
-        };
-        chunk_loop_dma<NTT_WAVES>(in, npoly, nunits, ppw, lds_addr(buf), L.lane, !LT::BIG, prologue, read, front,
-                                  back);
-    } else {
-        auto process = [&](uint32_t (&r)[32], uint32_t u) {
-            front(r, u);
-            back(r, u);
-        };
-        chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
-    }
+    auto process = [&](uint32_t (&r)[32], uint32_t u) {
+        front(r, u);
+        back(r, u);
+    };
+    chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
 }
 
 // out[t] = in[brv(t)] per polynomial, any 32-bit words: the pass-1
@@ -701,9 +607,8 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_bitrev(const uin
     uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
     auto load = [&](uint32_t (&r)[32], uint32_t u) {
-        const uint32_t poly = L.poly(u);
-        load32<P>(r, in + (size_t)poly * P::N + L.brl + (LT::BIG ? 32 * L.h : 0u), LT::BIG || poly < npoly,
-                  [](int j) { return p1s_off<P>(j); });
+        load32(r, in + (size_t)L.load_poly(u, npoly) * P::N + L.brl + (LT::BIG ? 32 * L.h : 0u),
+               [](int j) { return p1s_off<P>(j); });
     };
     auto process = [&](uint32_t (&r)[32], uint32_t u) {
         lds_p1_to_p2<P>(r, buf, L);
@@ -747,10 +652,11 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
         const uint32_t poly = L.poly(u);
         const bool valid = poly < npoly;
         const size_t off = (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
+        const size_t loff = (size_t)L.load_poly(u, npoly) * P::N + L.brl;
         // a first, then b: the transpose's memory fences keep b's loads below
         // a's transform, so only ~64 coefficients are live at the peak
         uint32_t ra[32], rb[32];
-        load32<P>(ra, a + off, valid, [](int j) { return LT::S * j; });
+        load32(ra, a + loff, [](int j) { return LT::S * j; });
         fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
         lds_p1_to_p2<P>(ra, buf, L);
         fwd_pass2<P>(ra, ftw2 + opaque_zero(), L.lane);
@@ -759,7 +665,7 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
             ra[j] = umin(ra[j], ra[j] - P::Q2);
             // b-hat is in natural order: register j of the pass-2 layout holds
             // index brv5(j)*S + lane (the forward's store mapping)
-            rb[j] = valid ? ld_in(b + off + LT::S * (BHAT ? brv5(j) : (uint32_t)j)) : 0u;
+            rb[j] = ld_in(b + loff + LT::S * (BHAT ? brv5(j) : (uint32_t)j));
         }
         if constexpr (!BHAT) {
             fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());

@@ -3,7 +3,6 @@
 // include/qtesla_ntt.h.  The kernels themselves are in ntt_device.hpp.
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -54,24 +53,9 @@ struct DevInfo {
     bool tables = false;
     bool geo = false;
     int cus = 256;
-    int wg_per_cu = 2;   // k_ntt_fwd/inv workgroups resident per CU (LDS-capped)
 };
 std::mutex g_dev_mutex;
 DevInfo g_dev[kMaxDev];
-
-// Prefetch policy of the transforms (see chunk_loop_dma): -1 = automatic,
-// 0 = never, 1 = always.  Initial value from QTESLA_NTT_PREFETCH (0/1),
-// changed by ntt_set_prefetch() (A/B, tuning, tests of both work loops).
-std::atomic<int> g_prefetch{[] {
-    const char *e = getenv("QTESLA_NTT_PREFETCH");
-    if (!e || !*e) return -1;
-    return atoi(e) ? 1 : 0;
-}()};
-int prefetch_policy() { return g_prefetch.load(std::memory_order_relaxed); }
-// automatic: the prefetch loop for grids of at most this many workgroup rounds
-#ifndef NTT_PF_MAX_ROUNDS
-#define NTT_PF_MAX_ROUNDS 2
-#endif
 
 // Current device, checked, with tables uploaded and geometry known.
 int device_ready(DevInfo **out)
@@ -86,10 +70,6 @@ int device_ready(DevInfo **out)
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return hip_err(e);
         d.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_ntt_fwd<2, false, false>, NTT_WG, 0) == hipSuccess &&
-            nb > 0)
-            d.wg_per_cu = nb;
         d.geo = true;
     }
     if (!d.tables) {
@@ -112,7 +92,6 @@ int device_ready(DevInfo **out)
 #endif
 struct Launch {
     uint32_t grid, ppw;
-    bool prefetch;
 };
 enum Op { OP_XFORM, OP_MUL };
 Launch launch_for(Op op, int ps, size_t npoly, const DevInfo &d)
@@ -126,9 +105,6 @@ Launch launch_for(Op op, int ps, size_t npoly, const DevInfo &d)
     Launch l;
     l.grid = (uint32_t)((units + waves * ppw - 1) / (waves * ppw));
     l.ppw = (uint32_t)ppw;
-    const int pol = prefetch_policy();
-    l.prefetch = op == OP_XFORM &&
-                 (pol == 1 || (pol < 0 && l.grid <= (size_t)NTT_PF_MAX_ROUNDS * d.cus * d.wg_per_cu));
     return l;
 }
 
@@ -178,16 +154,10 @@ template <int PS> struct LXform {
         const dim3 g(l.grid), b(NTT_WG);
         const uint32_t nb = (uint32_t)batch;
         switch (k) {
-        case FWD:
-            if (l.prefetch) hipLaunchKernelGGL((k_ntt_fwd<PS, false, true>), g, b, 0, s, in, out, nb, l.ppw);
-            else hipLaunchKernelGGL((k_ntt_fwd<PS, false, false>), g, b, 0, s, in, out, nb, l.ppw);
-            break;
-        case INV:
-            if (l.prefetch) hipLaunchKernelGGL((k_ntt_inv<PS, false, true>), g, b, 0, s, in, out, nb, l.ppw);
-            else hipLaunchKernelGGL((k_ntt_inv<PS, false, false>), g, b, 0, s, in, out, nb, l.ppw);
-            break;
-        case FWD_BR: hipLaunchKernelGGL((k_ntt_fwd<PS, true, false>), g, b, 0, s, in, out, nb, l.ppw); break;
-        case INV_BR: hipLaunchKernelGGL((k_ntt_inv<PS, true, false>), g, b, 0, s, in, out, nb, l.ppw); break;
+        case FWD: hipLaunchKernelGGL((k_ntt_fwd<PS, false>), g, b, 0, s, in, out, nb, l.ppw); break;
+        case INV: hipLaunchKernelGGL((k_ntt_inv<PS, false>), g, b, 0, s, in, out, nb, l.ppw); break;
+        case FWD_BR: hipLaunchKernelGGL((k_ntt_fwd<PS, true>), g, b, 0, s, in, out, nb, l.ppw); break;
+        case INV_BR: hipLaunchKernelGGL((k_ntt_inv<PS, true>), g, b, 0, s, in, out, nb, l.ppw); break;
         case BITREV: hipLaunchKernelGGL(k_bitrev<PS>, g, b, 0, s, in, out, nb, l.ppw); break;
         }
         return finish_launch();
@@ -377,11 +347,7 @@ int ntt_fill_uniform(uint32_t *d_poly, size_t batch, int ps, uint64_t seed, uint
 
 int ntt_last_hip_error(void) { return t_last_hip; }
 
-int ntt_set_prefetch(int policy)
-{
-    if (policy < -1 || policy > 1) return NTT_ERR_PARAM;
-    return g_prefetch.exchange(policy);
-}
+
 
 const char *ntt_strerror(int code)
 {
@@ -406,7 +372,7 @@ int ntt_build_info(char *buf, size_t len)
     static const char *s =
         "qtesla_ntt gfx950: 1 launch/op, wave-per-poly (n=2048) / half-wave-per-poly (n=1024), 32 coeff/lane, "
         "LDS XOR-swizzled transpose, permlane32 bit-5 stage, Shoup/Harvey lazy CT + signed-Shoup GS butterflies, "
-        "LDS-DMA prefetch at <= " QNTT_STR(NTT_PF_MAX_ROUNDS) " workgroup rounds; wg=" QNTT_STR(NTT_WG)
+        "dispatch-ordered unit chunks; wg=" QNTT_STR(NTT_WG)
         " mul_wg=" QNTT_STR(MUL_WG) "/" QNTT_STR(MUL_WG_BIG) " ppw<=" QNTT_STR(NTT_PPW_MAX)
         " min_wg/cu=" QNTT_STR(NTT_MIN_WG_PER_CU) "; src=" QNTT_SRC_HASH;
     const int n = (int)strlen(s);

@@ -87,7 +87,6 @@ def lib():
         L.poly_mul_nussbaumer.argtypes = [_vp, _vp, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp]
         L.ntt_fill_uniform.argtypes = [_vp, _sz, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp]
         L.ntt_last_hip_error.restype = ctypes.c_int
-        L.ntt_set_prefetch.argtypes = [ctypes.c_int]
         L.ntt_strerror.restype = ctypes.c_char_p
         L.ntt_strerror.argtypes = [ctypes.c_int]
         L.ntt_build_info.argtypes = [ctypes.c_char_p, _sz]
@@ -130,15 +129,6 @@ def build_info() -> str:
     buf = ctypes.create_string_buffer(1024)
     lib().ntt_build_info(buf, 1024)
     return buf.value.decode()
-
-
-def set_prefetch(policy: int) -> int:
-    """Work loop of the transforms: -1 automatic, 0 never, 1 always prefetch
-    (ntt_set_prefetch); returns the previous policy."""
-    rc = lib().ntt_set_prefetch(int(policy))
-    if rc < -1:
-        raise NTTError(rc, "ntt_set_prefetch")
-    return rc
 
 
 def build_hash() -> str:

@@ -3,7 +3,7 @@
 // of csrc/ntt_device.hpp next to variants that keep one side of them only.
 // Never linked into libqtesla_ntt.so; used by tools/variants.py.
 //
-//   variant 0  full kernel (k_ntt_fwd / k_ntt_inv, natural order, no prefetch)
+//   variant 0  full kernel (k_ntt_fwd / k_ntt_inv, natural order)
 //   variant 1  global load + store only (same addresses, grid and work loop)
 //   variant 2  arithmetic + LDS transposes only (no global memory)
 //   variant 3  load + LDS transpose(s) + store (no arithmetic)
@@ -39,13 +39,12 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_variant(const ui
     uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
     auto load = [&](uint32_t (&r)[32], uint32_t u) {
-        const uint32_t poly = L.poly(u);
         if constexpr (V == 2) {
 #pragma unroll
             for (int j = 0; j < 32; ++j) r[j] = L.lane * (j + u);
         } else {
-            load32<P>(r, in + (size_t)poly * P::N + L.brl, LT::BIG || poly < npoly,
-                      [](int j) { return INV ? brv5(j) * LT::S : LT::S * j; });
+            load32(r, in + (size_t)L.load_poly(u, npoly) * P::N + L.brl,
+                   [](int j) { return INV ? brv5(j) * LT::S : LT::S * j; });
         }
     };
     auto process = [&](uint32_t (&r)[32], uint32_t u) {
@@ -111,11 +110,11 @@ int launch(int op, int variant, uint32_t *out, const uint32_t *in, uint32_t nb, 
     const dim3 g((units + NTT_WAVES * ppw - 1) / (NTT_WAVES * ppw)), b(NTT_WG);
 #define QNTT_V(INV, V) hipLaunchKernelGGL((k_variant<PS, INV, V>), g, b, 0, s, in, out, nb, ppw)
     switch (op * 16 + variant) {
-    case 0: hipLaunchKernelGGL((k_ntt_fwd<PS, false, false>), g, b, 0, s, in, out, nb, ppw); break;
+    case 0: hipLaunchKernelGGL((k_ntt_fwd<PS, false>), g, b, 0, s, in, out, nb, ppw); break;
     case 1: QNTT_V(false, 1); break;
     case 2: QNTT_V(false, 2); break;
     case 3: QNTT_V(false, 3); break;
-    case 16: hipLaunchKernelGGL((k_ntt_inv<PS, false, false>), g, b, 0, s, in, out, nb, ppw); break;
+    case 16: hipLaunchKernelGGL((k_ntt_inv<PS, false>), g, b, 0, s, in, out, nb, ppw); break;
     case 17: QNTT_V(true, 1); break;
     case 18: QNTT_V(true, 2); break;
     case 19: QNTT_V(true, 3); break;

@@ -35,9 +35,6 @@ def test_error_codes_before_any_gpu_work(ntt):
     assert L.poly_ntt(fake, None, 1 << 31, 2, None) == ntt.NTT_ERR_SIZE
     assert L.poly_ntt_bitrev(fake, fake + 4, 2, 0, None) == ntt.NTT_ERR_ALIAS
     assert L.poly_invntt_bitrev(None, fake, 1, 2, None) == ntt.NTT_ERR_NULL
-    assert L.ntt_set_prefetch(2) == ntt.NTT_ERR_PARAM
-    old = ntt.set_prefetch(0)
-    assert ntt.set_prefetch(old) == 0
     for code in (0, -1, -2, -3, -4, -5, -6):
         assert L.ntt_strerror(code)
     with pytest.raises(KeyError):

@@ -42,17 +42,9 @@ def test_golden_vectors(ntt, oracle, dev, ps):
     assert np.array_equal(_u32(ntt, t)[0], g["pattern"])
 
 
-@pytest.fixture(params=[-1, 0, 1], ids=["loop-auto", "loop-plain", "loop-prefetch"])
-def prefetch(request, ntt):
-    """Run the test under each work-loop policy of the transforms (ntt_set_prefetch)."""
-    old = ntt.set_prefetch(request.param)
-    yield request.param
-    ntt.set_prefetch(old)
-
-
 @pytest.mark.parametrize("ps", PARAM_SETS)
 @pytest.mark.parametrize("batch", [1, 2, 3, 64, 257, 8195])
-def test_fwd_inv_random(ntt, oracle, dev, ps, batch, prefetch):
+def test_fwd_inv_random(ntt, oracle, dev, ps, batch):
     x = oracle.fill_uniform(batch, ps, 0xC0FFEE + batch, 0)
     t = _dev(ntt, x, dev)
     ntt.poly_ntt(t, ps)
