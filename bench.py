@@ -1,22 +1,39 @@
 #!/usr/bin/env python3
 """Benchmark of the north-star path: batched forward + inverse negacyclic NTT,
-n = 2048, qTESLA-p-III (q = 856145921), batch = 2^20 polynomials per GPU.
+n = 2048, qTESLA-p-III (q = 856145921), batch = 2^20 polynomials per GPU
+(BASELINE.json config 3, the default), and the other BASELINE configs:
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+    python bench.py [--gpus N] [--steps K] [--warmup W]          # config 3
+    python bench.py --config {1,2,3,4,5} ...                      # BASELINE configs
+    torchrun --nproc-per-node N bench.py --gpus N ...             # one rank per GPU
 
-A step = poly_ntt + poly_invntt, in place, over the rank's whole batch (inputs
-resident in HBM, generated on the device).  Polynomials are independent, so
-the batch shards with no data-path collective: rank r owns polys
-[r*B, (r+1)*B) of one global counter-based input stream ("weak" scaling).
-torch.distributed (RCCL) is used only for the barrier and the max-over-ranks
-time.  Rank 0 prints ONE JSON line.
+  config 1  single forward NTT n=1024 p-I: the reference's serial CPU path
+            (plumbing); the GPU line is the batch-1 launch latency
+  config 2  forward NTT n=1024 p-I, batch 65536
+  config 3  forward + inverse NTT n=2048 p-III, batch 2^20 (headline)
+  config 4  fused negacyclic poly-mul n=2048 p-III, 2^20 per GPU (2^23 on 8)
+  config 5  Nussbaumer negacyclic product n=2048 p-III, 2^20 (mod q)
+
+A step = one pass of the configured operation over the rank's whole batch
+(inputs resident in HBM, generated on the device; the transforms in place,
+as the reference's kernels).  Polynomials are independent, so the batch
+shards with no data-path collective: rank r owns polys [r*B, (r+1)*B) of one
+global counter-based input stream ("weak" scaling).  torch.distributed
+(RCCL, or gloo with --dist-backend gloo) is used only for the barrier and the
+max-over-ranks time.  Rank 0 prints ONE JSON line.
 
 Roofline: the dominant kernel's average launch duration is measured with HIP
 events on the stream the kernels run on; achieved = algorithmic bytes per
-launch (8 B per coefficient: one read + one write) / that duration.
-cpu_baseline: the oracle's restatement of the reference's serial CPU NTT
-(NTT.cu radix2NTT / radix2INTTGS with % q) on this host, rank 0, N = 1 only.
+launch (8 B per coefficient for a transform, 12 B for a product) / that
+duration.  traffic = measured HBM bytes per launch from
+profiles/pmc_summary.json, only when it was taken on this library build.
+
+After the timed region, outside it (the checker legs, like cpu_baseline):
+the transform round trip over the whole batch on device, and >= 64 sampled
+polynomials of one more launch on the regenerated input compared with the
+CPU oracle (oracle/, test infrastructure; never the measured path).
+cpu_baseline: the oracle's restatement of the reference's serial CPU path
+for the same operation, on this host, rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -32,6 +49,19 @@ sys.path.insert(0, os.path.join(ROOT, "ntt-gpu-qtesla_amd"))
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "NTTs/sec (fwd+inv, n=2048 qTESLA-p-III) at batch=2^20; achieved HBM GB/s"
 SEED = 0x5EED0003
+PMC_PATH = os.path.join(ROOT, "profiles", "pmc_summary.json")
+
+# BASELINE.json configs -> (op, param, batch per GPU, ring)
+CONFIGS = {
+    1: ("fwd", "p-I", 1, "q"),
+    2: ("fwd", "p-I", 65536, "q"),
+    3: ("fwdinv", "p-III", 1 << 20, "q"),
+    4: ("polymul", "p-III", 1 << 20, "q"),
+    5: ("nussbaumer", "p-III", 1 << 20, "q"),
+}
+OPS = ["fwdinv", "fwd", "inv", "polymul", "polymul_ntt", "nussbaumer", "polymul_host", "fwdinv_host"]
+UNIT = {"fwdinv": "fwd+inv pairs/s", "fwd": "NTTs/s", "inv": "INTTs/s", "polymul": "products/s",
+        "polymul_ntt": "products/s", "nussbaumer": "products/s"}
 
 
 def shard(total_per_rank: int, rank: int) -> tuple[int, int]:
@@ -46,71 +76,107 @@ def dist_env():
     return rank, world, local
 
 
-def max_over_ranks(value: float, world: int, device=None) -> float:
-    if world <= 1:
-        return value
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([value], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+class Dist:
+    """The only collectives of the bench: barrier and max over ranks."""
 
+    def __init__(self, world: int, backend: str, device):
+        self.world, self.backend, self.device = world, backend, device
+        if world > 1:
+            import torch.distributed as dist
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=device)
+            else:
+                dist.init_process_group("gloo")
 
-def barrier(world: int, device=None):
-    if world > 1:
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def max(self, value: float) -> float:
+        if self.world <= 1:
+            return value
+        import torch
         import torch.distributed as dist
-        if device is not None and device.type == "cuda":
-            dist.barrier(device_ids=[device.index])
-        else:
-            dist.barrier()
+        t = torch.tensor([value], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
 
 
-def cpu_baseline(param: str, seconds: float, threads: int = 1) -> dict:
-    """Reference serial CPU NTT restated in the oracle, timed on a bounded sample."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        return "unknown"
+
+
+def cpu_baseline(op: str, param: str, seconds: float, threads: int = 1, ring: str = "q", max_count=1 << 20) -> dict:
+    """The reference's serial CPU path for `op`, restated in the oracle, timed
+    on a bounded sample of the workload (about `seconds` of wall time)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     if not os.path.exists(O.LIB_PATH):
         O.build()
-    # scale the sample to ~`seconds` of wall time (two refinements: a tiny
-    # first sample under-estimates the per-poly time of a multi-thread run)
+    top = {"fwdinv": "fwdinv", "fwd": "fwd", "inv": "inv", "polymul": "polymul", "polymul_ntt": "polymul",
+           "nussbaumer": "nussbaumer_m32" if ring == "m32" else "nussbaumer_q"}[op]
     count = 8 * threads
-    for _ in range(3):
+    for _ in range(4):   # scale the sample to ~`seconds` (a tiny first sample under-estimates)
         x = O.fill_uniform(count, param, SEED, 0)
-        t = O.time_fwd_inv(x, param, threads, 1)
-        if t >= 0.5 * seconds or count >= (1 << 20):
+        y = O.fill_uniform(count, param, SEED ^ 0xFFFF, 0)
+        t = O.time_op(top, x, param, threads, 1, y=y)
+        if t >= 0.5 * seconds or count >= max_count:
             break
-        count = min(max(count, int(count * seconds / max(t, 1e-6))), 1 << 20)
+        count = min(max(count + 1, int(count * seconds / max(t, 1e-6))), max_count)
     n = O.params(param)["n"]
-    cpu = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
+    what = {"fwdinv": "fwd (Phi twist + bit_reverse_copy + radix2NTT) + inv (radix2INTTGS + bitrev + invPhi)",
+            "fwd": "fwd (Phi twist + bit_reverse_copy + radix2NTT, NTT.cu:1908-1926)",
+            "inv": "inv (radix2INTTGS + bitrev + invPhi)",
+            "polymul": "test_NTT_nega_CT composition: fwd(a), fwd(b), pointwise, inv (NTT.cu:1908-1946)",
+            "nussbaumer_m32": "nussbaumer_fft mod 2^32-1 (NTT.cu:167-277), m=32",
+            "nussbaumer_q": "nussbaumer_fft's algorithm mod q (NTT.cu:167-277), m=32"}[top]
     return {
         "value": count / t,
-        "cpu_model": cpu,
-        "nproc": os.cpu_count(),
-        "unit": "fwd+inv pairs/s",
+        "unit": UNIT.get(op, "units/s"),
         "cores": threads,
         "kind": "port",
-        "sample": f"{count} uniform n={n} {param} polys, fwd(Phi twist+bit_reverse_copy+radix2NTT)+"
-                  f"inv(radix2INTTGS+bitrev+invPhi) with % q, oracle C restatement of NTT.cu, "
-                  f"{threads} thread(s), {t:.1f} s",
+        "cpu_model": _cpu_model(),
+        "nproc": os.cpu_count(),
+        "sample": f"{count} uniform n={n} {param} polys: {what} with % q, oracle C restatement of NTT.cu, "
+                  f"{threads} thread(s), {t:.2f} s",
     }
 
 
-def load_pmc(workload: str):
-    """HBM traffic per launch from a committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def load_pmc(workload: str, build_hash: str):
+    """HBM traffic per launch from the committed rocprofv3 PMC summary, only
+    when it was measured on this exact library build (else None + why)."""
     try:
-        with open(path) as f:
+        with open(PMC_PATH) as f:
             d = json.load(f)
-        if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None, "no profiles/pmc_summary.json"
+    e = d.get("entries", {}).get(workload)
+    if e is None:
+        return None, "no PMC entry for this workload"
+    if e.get("build_hash") != build_hash:
+        return None, f"PMC entry measured on build {e.get('build_hash')}, this library is {build_hash}"
+    return e.get("hbm_bytes_per_launch"), "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, this build"
+
+
+def workload_name(op, param, n, q, ring):
+    base = {"fwdinv": "fwd+inv negacyclic NTT", "fwd": "forward negacyclic NTT", "inv": "inverse negacyclic NTT",
+            "polymul": "fused negacyclic poly-mul",
+            "polymul_ntt": "fused negacyclic poly-mul, second operand in the NTT domain",
+            "nussbaumer": "Nussbaumer negacyclic product" + (" mod 2^32-1" if ring == "m32" else "")}[op]
+    return f"{base} n={n} qTESLA-{param}" if param != "ref" else f"{base} n={n} ref q={q}"
 
 
 def main():
@@ -118,19 +184,26 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--param", default="p-III")
-    ap.add_argument("--batch", type=int, default=1 << 20, help="polynomials per GPU")
-    ap.add_argument("--op", default="fwdinv",
-                    choices=["fwdinv", "fwd", "inv", "polymul", "polymul_ntt", "nussbaumer", "polymul_host",
-                             "fwdinv_host"])
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
+                    help="BASELINE.json config (sets op / param / batch defaults)")
+    ap.add_argument("--op", default=None, choices=OPS)
+    ap.add_argument("--param", default=None, choices=["ref", "p-I", "p-III"])
+    ap.add_argument("--batch", type=int, default=None, help="polynomials per GPU")
+    ap.add_argument("--ring", default=None, choices=["q", "m32"], help="--op nussbaumer: mod q or mod 2^32-1")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for the barrier / max-over-ranks (no data-path collective)")
     ap.add_argument("--pageable", action="store_true", help="*_host ops: pageable instead of pinned host buffers")
     ap.add_argument("--chunk", type=int, default=0, help="*_host ops: polys per chunk (0 = library default)")
     ap.add_argument("--slots", type=int, default=0, help="*_host ops: buffer slots (0 = library default)")
-    ap.add_argument("--ring", default="q", choices=["q", "m32"], help="--op nussbaumer: mod q or mod 2^32-1")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     args = ap.parse_args()
+    c_op, c_param, c_batch, c_ring = CONFIGS[args.config]
+    args.op = args.op or c_op
+    args.param = args.param or c_param
+    args.batch = args.batch or c_batch
+    args.ring = args.ring or c_ring
 
     import torch
     import ntt_amd
@@ -140,17 +213,14 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+    dist = Dist(world, args.dist_backend, device)
 
     if args.op.endswith("_host"):
-        return bench_host(args, ntt_amd, torch, device, rank, world)
+        return bench_host(args, ntt_amd, torch, device, rank, world, dist)
 
     pinfo = ntt_amd.param_info(args.param)
     n = pinfo["n"]
-    B = args.batch
-    first, count = shard(B, rank)
+    first, count = shard(args.batch, rank)
     x = torch.empty(count * n, dtype=torch.int32, device=device)
     ntt_amd.fill_uniform(x, args.param, SEED, first)
     y = z = None
@@ -182,7 +252,7 @@ def main():
 
     evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in kinds]
            for _ in range(args.steps)]
-    barrier(world, device)
+    dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for s in range(args.steps):
@@ -192,8 +262,8 @@ def main():
             evs[s][i][1].record(stream)
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
-    barrier(world, device)
-    elapsed = max_over_ranks(t1 - t0, world, device)
+    dist.barrier()
+    elapsed = dist.max(t1 - t0)
 
     per_kind = {k: sum(evs[s][i][0].elapsed_time(evs[s][i][1]) for s in range(args.steps)) / args.steps
                 for i, k in enumerate(kinds)}  # ms per launch
@@ -202,28 +272,22 @@ def main():
     alg_bytes = count * n * bytes_per_coeff
     achieved = alg_bytes / (per_kind[dom] * 1e-3) / 1e9
 
-    ok = None
+    check = {"roundtrip_identity_full_batch": None, "sampled_vs_oracle": None}
     if not args.no_check:
-        if args.op in ("fwdinv",):
-            # every step is the identity: the buffer must equal the regenerated input
-            ref = torch.empty_like(x)
-            ntt_amd.fill_uniform(ref, args.param, SEED, first)
-            ok = bool(torch.equal(ref, x))
-            del ref
-        ok = bool(max_over_ranks(0.0 if ok in (None, True) else 1.0, world, device) == 0.0) if ok is not None else None
+        check = checker_legs(args, ntt_amd, torch, x, y, z, first, count, n)
+        bad = 0.0 if all(v is None or v is True or (isinstance(v, dict) and v.get("ok")) for v in check.values()) \
+            else 1.0
+        check["all_ranks_ok"] = dist.max(bad) == 0.0
 
     units = world * count * args.steps
     value = units / elapsed
-    workload = {"fwdinv": "fwd+inv negacyclic NTT", "fwd": "forward negacyclic NTT",
-                "inv": "inverse negacyclic NTT", "polymul": "fused negacyclic poly-mul",
-                "polymul_ntt": "fused negacyclic poly-mul, second operand in the NTT domain",
-                "nussbaumer": "Nussbaumer negacyclic product" + (" mod 2^32-1" if args.ring == "m32" else "")}[args.op]
-    workload = f"{workload} n={n} qTESLA-{args.param}" if args.param != "ref" else f"{workload} n={n} ref q={pinfo['q']}"
-    unit = {"fwdinv": "fwd+inv pairs/s", "fwd": "NTTs/s", "inv": "INTTs/s", "polymul": "products/s",
-            "polymul_ntt": "products/s",
-            "nussbaumer": "products/s"}[args.op]
+    workload = workload_name(args.op, args.param, n, pinfo["q"], args.ring)
+    unit = UNIT[args.op]
+    build_hash = ntt_amd.build_hash()
+    traffic, traffic_note = load_pmc(workload, build_hash)
+    headline = args.op == "fwdinv" and args.param == "p-III" and args.batch == 1 << 20
     out = {
-        "metric": METRIC if args.op == "fwdinv" and args.param == "p-III" else f"{unit} ({workload})",
+        "metric": METRIC if headline else f"{unit} ({workload}, batch {args.batch} per GPU)",
         "value": value,
         "unit": unit,
         "n_gpus": world,
@@ -235,39 +299,109 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (device counter-based uniform coefficients in [0,q))",
-        "config": {"workload": workload, "param_set": args.param, "n": n, "q": pinfo["q"],
-                   "batch_per_gpu": count, "global_batch": world * count, "parallelism": f"batch-shard x{world}"},
+        "config": {"workload": workload, "baseline_config": args.config if (args.op, args.param, args.batch) ==
+                   CONFIGS[args.config][:3] else None, "param_set": args.param, "n": n, "q": pinfo["q"],
+                   "batch_per_gpu": count, "global_batch": world * count, "parallelism": f"batch-shard x{world}",
+                   "dist_backend": args.dist_backend if world > 1 else None},
         "hbm_gbs_algorithmic": value * n * (bytes_per_coeff if args.op != "fwdinv" else 16) / 1e9,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_pmc(workload),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                      "avg_launch_ms": per_kind[dom], "alg_bytes_per_launch": alg_bytes,
                      "per_kernel_ms": per_kind},
-        "check": {"roundtrip_identity_full_batch": ok},
+        "check": check,
+        "build": {"hash": build_hash},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.param, args.cpu_seconds, 1)
-        # the same restatement batch-parallel over this box's CPU share
-        threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-        out["cpu_baseline_all_cores"] = cpu_baseline(args.param, args.cpu_seconds / 2, threads)
+        out.update(cpu_baseline_legs(args, n))
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
-    if ok is False:
+    dist.close()
+    if not args.no_check and not check.get("all_ranks_ok", True):
         sys.exit(1)
 
 
-def bench_host(args, ntt_amd, torch, device, rank, world):
+def cpu_baseline_legs(args, n):
+    """cpu_baseline (1 thread, the reference is serial) and the same path
+    batch-parallel over this box's CPU share."""
+    out = {}
+    if args.config == 1 and args.op == "fwd":
+        # config 1: the serial single forward of main.cu, for p-I and the
+        # reference's own set (BASELINE's q differs from main.cu's)
+        out["cpu_baseline"] = cpu_baseline("fwd", args.param, args.cpu_seconds, 1)
+        other = "ref" if args.param != "ref" else "p-I"
+        out[f"cpu_baseline_{other}"] = cpu_baseline("fwd", other, args.cpu_seconds / 2, 1)
+        return out
+    out["cpu_baseline"] = cpu_baseline(args.op, args.param, args.cpu_seconds, 1, args.ring)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    out["cpu_baseline_all_cores"] = cpu_baseline(args.op, args.param, args.cpu_seconds / 2, threads, args.ring)
+    if args.op == "nussbaumer":
+        # the reference's own Nussbaumer shape: test_nussbaumer, n=1024 mod 2^32-1 (NTT.cu:1987-2005)
+        out["cpu_baseline_reference_shape"] = cpu_baseline("nussbaumer", "p-I", args.cpu_seconds / 2, 1, "m32")
+    return out
+
+
+def checker_legs(args, ntt_amd, torch, x, y, z, first, count, n):
+    """Correctness legs, outside the timed region.  The oracle (oracle/, the
+    CPU restatement of NTT.cu) is only the checker here, as in the tests."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    if not os.path.exists(O.LIB_PATH):
+        O.build()
+    ps = args.param
+    res = {"roundtrip_identity_full_batch": None}
+    rng = np.random.default_rng(first + 1)
+    idx = np.unique(np.concatenate([[0, count - 1], rng.integers(0, count, 62)])) if count > 64 \
+        else np.arange(count)
+    tidx = torch.as_tensor(idx, device=x.device)
+
+    def host(seed, i):   # the device generator's polys, regenerated on the host
+        return np.concatenate([O.fill_uniform(1, ps, seed, first + int(k)) for k in i])
+
+    def sample(t):
+        return ntt_amd.to_numpy_u32(t.view(count, n)[tidx])
+
+    if args.op == "fwdinv":
+        # every step is the identity: the buffer must equal the regenerated input
+        ref = torch.empty_like(x)
+        ntt_amd.fill_uniform(ref, ps, SEED, first)
+        res["roundtrip_identity_full_batch"] = bool(torch.equal(ref, x))
+        del ref
+    a = host(SEED, idx)
+    if args.op in ("fwdinv", "fwd", "inv"):
+        # one more launch on the regenerated input, sampled polys vs the oracle
+        ntt_amd.fill_uniform(x, ps, SEED, first)
+        if args.op == "inv":
+            ntt_amd.poly_invntt(x, ps)
+            want = O.poly_invntt(a, ps)
+        else:
+            ntt_amd.poly_ntt(x, ps)
+            want = O.poly_ntt(a, ps)
+        got = sample(x)
+    else:
+        b = host(SEED ^ 0xFFFF, idx)
+        got = sample(z)
+        if args.op == "polymul":
+            want = O.poly_mul(a, b, ps)
+        elif args.op == "polymul_ntt":   # y is taken as b-hat: c = a * INTT(b-hat)
+            want = O.poly_mul(a, O.poly_invntt(b, ps), ps)
+        elif args.ring == "m32":
+            want = O.m32_canon(O.nussbaumer(a, b, n, "m32"))
+        else:
+            want = O.poly_mul(a, b, ps)
+    res["sampled_vs_oracle"] = {"polys": int(len(idx)), "ok": bool(np.array_equal(got.reshape(want.shape), want))}
+    return res
+
+
+def bench_host(args, ntt_amd, torch, device, rank, world, dist):
     """Host -> host operation through ntt_host_ctx: the
     reference's PCIe-inclusive timing (NTT.cu:2384-2428), pipelined.  Never
     the headline `value` of the device-resident metric."""
     import numpy as np
     pinfo = ntt_amd.param_info(args.param)
     n = pinfo["n"]
-    B = args.batch
-    first, count = shard(B, rank)
+    first, count = shard(args.batch, rank)
     nin = 2 if args.op == "polymul_host" else 1
 
     def host_buf(seed):
@@ -292,13 +426,13 @@ def bench_host(args, ntt_amd, torch, device, rank, world):
 
     for _ in range(args.warmup):
         step()
-    barrier(world, device)
+    dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     t1 = time.perf_counter()
-    barrier(world, device)
-    elapsed = max_over_ranks(t1 - t0, world, device)
+    dist.barrier()
+    elapsed = dist.max(t1 - t0)
     ok = None
     if not args.no_check:
         ok = bool(np.array_equal(c, a)) if nin == 1 else None
@@ -323,9 +457,7 @@ def bench_host(args, ntt_amd, torch, device, rank, world):
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    dist.close()
 
 
 if __name__ == "__main__":

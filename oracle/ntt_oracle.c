@@ -506,30 +506,51 @@ void oracle_fill_uniform(uint32_t *x, size_t batch, int ps, uint64_t seed, uint6
 }
 
 /* ----------------------- CPU baseline timing ------------------------ */
+/* The reference's serial CPU paths restated above, timed over a batch split
+ * across pthreads (CPU baseline of bench.py; never the product path):
+ *   ORACLE_OP_FWDINV  FWD + INV (E4 test_NTT_nega_CT path, NTT.cu:1908-1946)
+ *   ORACLE_OP_FWD     FWD only (twist + bit_reverse_copy + radix2NTT)
+ *   ORACLE_OP_INV     INV only (radix2INTTGS + bitrev + invPhi)
+ *   ORACLE_OP_POLYMUL FWD(a), FWD(b), pointwise, INV  (oracle_poly_mul)
+ *   ORACLE_OP_NUS_M32 nussbaumer_fft (NTT.cu:167-277) mod 2^32-1
+ *   ORACLE_OP_NUS_Q   the same algorithm mod q                              */
 typedef struct {
-    uint32_t *x;
+    int op, ps, reps;
+    uint32_t *x, *y, *z;
     size_t batch;
-    int ps, reps;
     const tabset *t;
 } job;
 
 static void *run_job(void *arg)
 {
     job *j = (job *)arg;
-    uint32_t *tmp = (uint32_t *)malloc(4 * (size_t)j->t->p.n);
+    const uint32_t n = j->t->p.n;
+    uint32_t *tmp = (uint32_t *)malloc(4 * (size_t)n);
     for (int r = 0; r < j->reps; r++) {
-        poly_ntt_with(j->x, j->batch, j->ps, j->t, tmp);
-        poly_invntt_with(j->x, j->batch, j->ps, j->t, tmp);
+        switch (j->op) {
+        case ORACLE_OP_FWDINV:
+            poly_ntt_with(j->x, j->batch, j->ps, j->t, tmp);
+            poly_invntt_with(j->x, j->batch, j->ps, j->t, tmp);
+            break;
+        case ORACLE_OP_FWD: poly_ntt_with(j->x, j->batch, j->ps, j->t, tmp); break;
+        case ORACLE_OP_INV: poly_invntt_with(j->x, j->batch, j->ps, j->t, tmp); break;
+        case ORACLE_OP_POLYMUL: oracle_poly_mul(j->z, j->x, j->y, j->batch, j->ps); break;
+        case ORACLE_OP_NUS_M32: oracle_nussbaumer(j->z, j->x, j->y, j->batch, n, 0); break;
+        case ORACLE_OP_NUS_Q: oracle_nussbaumer(j->z, j->x, j->y, j->batch, n, j->t->p.q); break;
+        }
     }
     free(tmp);
     return NULL;
 }
 
-/* Times reps x (FWD + INV) over `batch` polys split across `threads`
- * pthreads.  Returns wall seconds (CLOCK_MONOTONIC). */
-double oracle_time_fwd_inv(uint32_t *x, size_t batch, int ps, int threads, int reps)
+/* Times `reps` passes of `op` over `batch` polys (x, and y/z for the
+ * products) split across `threads` pthreads.  Returns wall seconds
+ * (CLOCK_MONOTONIC), or -1 on a bad argument. */
+double oracle_time_op(int op, uint32_t *x, uint32_t *y, uint32_t *z, size_t batch, int ps, int threads, int reps)
 {
     tabset t;
+    if (op < ORACLE_OP_FWDINV || op > ORACLE_OP_NUS_Q) return -1.0;
+    if (op >= ORACLE_OP_POLYMUL && (!y || !z)) return -1.0;
     if (tabset_make(ps, &t)) return -1.0;
     if (threads < 1) threads = 1;
     pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
@@ -540,11 +561,8 @@ double oracle_time_fwd_inv(uint32_t *x, size_t batch, int ps, int threads, int r
     int used = 0;
     for (int i = 0; i < threads && start < batch; i++) {
         size_t cnt = (start + per <= batch) ? per : batch - start;
-        jobs[i].x = x + start * t.p.n;
-        jobs[i].batch = cnt;
-        jobs[i].ps = ps;
-        jobs[i].reps = reps;
-        jobs[i].t = &t;
+        const size_t off = start * t.p.n;
+        jobs[i] = (job){op, ps, reps, x + off, y ? y + off : NULL, z ? z + off : NULL, cnt, &t};
         pthread_create(&th[i], NULL, run_job, &jobs[i]);
         start += cnt;
         used++;
@@ -555,4 +573,9 @@ double oracle_time_fwd_inv(uint32_t *x, size_t batch, int ps, int threads, int r
     free(jobs);
     tabset_free(&t);
     return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+double oracle_time_fwd_inv(uint32_t *x, size_t batch, int ps, int threads, int reps)
+{
+    return oracle_time_op(ORACLE_OP_FWDINV, x, NULL, NULL, batch, ps, threads, reps);
 }

@@ -64,6 +64,9 @@ def lib():
             getattr(L, nm).argtypes = [_u32p, _u32p, _u32p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_m32_canon.restype = ctypes.c_uint32
         L.oracle_m32_canon.argtypes = [ctypes.c_uint32]
+        L.oracle_time_op.restype = ctypes.c_double
+        L.oracle_time_op.argtypes = [ctypes.c_int, _u32p, _u32p, _u32p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int]
         L.oracle_time_fwd_inv.restype = ctypes.c_double
         L.oracle_time_fwd_inv.argtypes = [_u32p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         _lib = L
@@ -184,6 +187,26 @@ def time_fwd_inv(x: np.ndarray, param_set, threads: int = 1, reps: int = 1) -> f
     n = params(param_set)["n"]
     y = _batched(x, n)
     return lib().oracle_time_fwd_inv(_ptr(y), y.size // n, _ps(param_set), threads, reps)
+
+
+TIME_OPS = {"fwdinv": 0, "fwd": 1, "inv": 2, "polymul": 3, "nussbaumer_m32": 4, "nussbaumer_q": 5}
+
+
+def time_op(op: str, x: np.ndarray, param_set, threads: int = 1, reps: int = 1, y: np.ndarray = None) -> float:
+    """Wall seconds of `reps` passes of the reference's serial CPU path `op`
+    (oracle_time_op) over the polys of x (and y for the products), split
+    across `threads` pthreads, on copies (the inputs are not modified)."""
+    n = params(param_set)["n"]
+    xa = _batched(x, n)
+    ya = za = None
+    if op in ("polymul", "nussbaumer_m32", "nussbaumer_q"):
+        ya = _batched(y, n)
+        za = np.zeros_like(xa)
+    t = lib().oracle_time_op(TIME_OPS[op], _ptr(xa), _ptr(ya) if ya is not None else None,
+                             _ptr(za) if za is not None else None, xa.size // n, _ps(param_set), threads, reps)
+    if t < 0:
+        raise ValueError(f"oracle_time_op({op}) failed")
+    return t
 
 
 M32 = 0xFFFFFFFF   # the reference's Nussbaumer ring Z/(2^32-1) (NTT.cu:102-134)

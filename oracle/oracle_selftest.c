@@ -44,6 +44,7 @@ int main(void)
         if (memcmp(d, z, 4 * n)) { printf("direct fail %d\n", ps); return 1; }
         oracle_pointwise(z, x, y, n * B, ps);
         oracle_time_fwd_inv(x, B, ps, 2, 1);
+        for (int op = ORACLE_OP_FWD; op <= ORACLE_OP_NUS_Q; op++) oracle_time_op(op, x, y, z, B, ps, 2, 1);
         free(x); free(y); free(c); free(d); free(yy); free(z);
         for (int i = 0; i < 5; i++) free(t[i]);
     }

@@ -103,7 +103,8 @@ def test_oracle_under_sanitizers(oracle, tmp_path):
     exe = tmp_path / "oracle_asan"
     r = subprocess.run(["gcc", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
                         "-std=c11", "-D_POSIX_C_SOURCE=200809L", "-o", str(exe),
-                        os.path.join(here, "oracle_selftest.c"), os.path.join(here, "ntt_oracle.c"), "-lpthread"],
+                        os.path.join(here, "oracle_selftest.c"), os.path.join(here, "ntt_oracle.c"),
+                        os.path.join(here, "nussbaumer_oracle.c"), "-lpthread"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300,
