@@ -150,12 +150,13 @@ def cpu_baseline(op: str, param: str, seconds: float, threads: int = 1, ring: st
         "kind": "port",
         "cpu_model": _cpu_model(),
         "nproc": os.cpu_count(),
-        "sample": f"{count} uniform n={n} {param} polys: {what} with % q, oracle C restatement of NTT.cu, "
+        "sample": f"{count} uniform n={n} {param} polys: {what}{'' if top == 'nussbaumer_m32' else ' with % q'}, "
+                  f"oracle C restatement of NTT.cu, "
                   f"{threads} thread(s), {t:.2f} s",
     }
 
 
-def load_pmc(workload: str, build_hash: str):
+def load_pmc(workload: str, batch: int, build_hash: str):
     """HBM traffic per launch from the committed rocprofv3 PMC summary, only
     when it was measured on this exact library build (else None + why)."""
     try:
@@ -166,6 +167,8 @@ def load_pmc(workload: str, build_hash: str):
     e = d.get("entries", {}).get(workload)
     if e is None:
         return None, "no PMC entry for this workload"
+    if e.get("batch") != batch:
+        return None, f"PMC entry measured at batch {e.get('batch')}"
     if e.get("build_hash") != build_hash:
         return None, f"PMC entry measured on build {e.get('build_hash')}, this library is {build_hash}"
     return e.get("hbm_bytes_per_launch"), "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, this build"
@@ -211,8 +214,11 @@ def main():
     rank, world, local = dist_env()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one rank per GPU; ranks beyond the visible devices share them (the
+    # world-size-2 rehearsal on a one-GPU box, with --dist-backend gloo)
+    dev_index = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     dist = Dist(world, args.dist_backend, device)
 
     if args.op.endswith("_host"):
@@ -284,7 +290,7 @@ def main():
     workload = workload_name(args.op, args.param, n, pinfo["q"], args.ring)
     unit = UNIT[args.op]
     build_hash = ntt_amd.build_hash()
-    traffic, traffic_note = load_pmc(workload, build_hash)
+    traffic, traffic_note = load_pmc(workload, count, build_hash)
     headline = args.op == "fwdinv" and args.param == "p-III" and args.batch == 1 << 20
     out = {
         "metric": METRIC if headline else f"{unit} ({workload}, batch {args.batch} per GPU)",

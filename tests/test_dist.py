@@ -6,7 +6,6 @@ import socket
 
 import numpy as np
 import pytest
-import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
@@ -25,15 +24,15 @@ def _worker(rank, world, port, out):
     sys.path[:0] = [root, os.path.join(root, "oracle")]
     import bench
     import oracle as O
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d = bench.Dist(world, "gloo", None)      # bench.py's process group (--dist-backend gloo)
     per = 3
     first, count = bench.shard(per, rank)
     x = O.fill_uniform(count, "p-I", 0x5EED0002, first)       # this rank's shard
     X = O.poly_ntt(x, "p-I")                                    # independent work, no exchange
-    bench.barrier(world)
-    t = bench.max_over_ranks(0.5 + rank, world)
+    d.barrier()
+    t = d.max(0.5 + rank)
     out[rank] = (first, count, t, X.tobytes())
-    dist.destroy_process_group()
+    d.close()
 
 
 def test_gloo_world2_sharding():

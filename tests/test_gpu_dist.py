@@ -1,0 +1,53 @@
+"""World-size-2 rehearsal of the multi-GPU path THROUGH the HIP library:
+two ranks (torch.distributed.run, gloo), each running ntt_amd on its shard of
+the batch -- on two GPUs when present, else both on the one device.  The
+8-GPU scaling run itself is the driver's (RCCL, one rank per GPU)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _torchrun(args, timeout=240):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}"] + args
+    env = {**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
+
+
+def test_shards_concatenate_to_single_process_result(ntt, tmp_path):
+    out = tmp_path / "dist.json"
+    r = _torchrun([os.path.join(ROOT, "tests", "dist_worker.py"), str(out)])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.loads(out.read_text())
+    assert set(res) == {"p-III", "p-I"}
+    for ps, v in res.items():
+        assert v["world"] == 2 and v["ntt"] and v["mul"], (ps, v)
+
+
+def test_bench_two_ranks_counts_both(ntt):
+    batch, steps = 8192, 3
+    r = _torchrun([os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", str(batch), "--steps", str(steps),
+                   "--warmup", "1", "--dist-backend", "gloo", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout        # rank 0 prints one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * batch
+    assert d["config"]["dist_backend"] == "gloo"
+    assert d["check"]["all_ranks_ok"] is True
+    # value = polys of BOTH ranks / the max-over-ranks wall time
+    assert abs(d["value"] - 2 * batch * steps / (d["ms_per_step"] * steps * 1e-3)) <= 1e-6 * d["value"]
