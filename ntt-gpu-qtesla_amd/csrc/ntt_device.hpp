@@ -50,6 +50,17 @@ __constant__ uint2 c_inv2[2048];
 // ------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
+// Conditional subtraction x >= C ? x - C : x, the lazy reductions (hipcc:
+// v_sub_u32 + v_min_u32).  A v_sub_co_u32 + v_cndmask_b32 form issues faster
+// in isolation (50 vs 36 lanes/clk/CU per pair, profiles/r02/valu_rates.log)
+// but its SGPR-mask hazards cost the same in the kernels: fwd / inv / poly_mul
+// unchanged within noise (profiles/r02/ab_csub.log).
+template <uint32_t C>
+__device__ __forceinline__ uint32_t csub(uint32_t x)
+{
+    return umin(x, x - C);
+}
+
 // low word of a*b + c (one v_mad_u64_u32)
 __device__ __forceinline__ uint32_t madlo32(uint32_t a, uint32_t b, uint32_t c)
 {
@@ -84,7 +95,7 @@ __device__ __forceinline__ uint32_t sshoup_mul(uint32_t d, uint32_t ws, uint32_t
 template <uint32_t Q, bool REDUCE = true>
 __device__ __forceinline__ void ct_bfly(uint32_t &x, uint32_t &y, uint32_t wn, uint32_t wp)
 {
-    const uint32_t a = REDUCE ? umin(x, x - 2 * Q) : x;   // [0,4q) -> [0,2q)
+    const uint32_t a = REDUCE ? csub<2 * Q>(x) : x;   // [0,4q) -> [0,2q)
     const uint32_t qe = __umulhi(y, wp);
     const uint32_t tn = madlo32(qe, Q, y * wn);           // -t, t in [0,2q)
     x = a - tn;
@@ -96,9 +107,8 @@ __device__ __forceinline__ void ct_bfly(uint32_t &x, uint32_t &y, uint32_t wn, u
 template <uint32_t Q>
 __device__ __forceinline__ void gs_bfly(uint32_t &x, uint32_t &y, uint32_t ws, uint32_t wps)
 {
-    uint32_t s = x + y;   // [0,4q)
-    s = umin(s, s - 2 * Q);
-    const uint32_t d = x - y;   // (-2q, 2q) as a signed value
+    const uint32_t s = csub<2 * Q>(x + y);   // [0,4q) -> [0,2q)
+    const uint32_t d = x - y;                 // (-2q, 2q) as a signed value
     x = s;
     y = sshoup_mul<Q>(d, ws, wps);
 }
@@ -117,8 +127,7 @@ __device__ __forceinline__ uint32_t mont_mul(uint32_t a, uint32_t b)
 template <class P>
 __device__ __forceinline__ uint32_t canon4(uint32_t x)
 {
-    x = umin(x, x - P::Q2);
-    return umin(x, x - P::Q);
+    return csub<P::Q>(csub<P::Q2>(x));
 }
 
 // ------------------------------------------------------------------------
@@ -410,8 +419,8 @@ __device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const u
         const uint32_t d = x - y;   // (-2q, 2q), signed
         const uint32_t a = shoup_mul<P::Q>(s, S0, S0P);
         const uint32_t b = sshoup_mul<P::Q>(d, S1S.x, S1S.y);
-        r[j] = umin(a, a - P::Q);
-        r[j + 16] = umin(b, b - P::Q);
+        r[j] = csub<P::Q>(a);
+        r[j + 16] = csub<P::Q>(b);
         emit(j, r[j]);
         emit(j + 16, r[j + 16]);
     }
@@ -662,7 +671,7 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
         fwd_pass2<P>(ra, ftw2 + opaque_zero(), L.lane);
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
-            ra[j] = umin(ra[j], ra[j] - P::Q2);
+            ra[j] = csub<P::Q2>(ra[j]);
             // b-hat is in natural order: register j of the pass-2 layout holds
             // index brv5(j)*S + lane (the forward's store mapping)
             rb[j] = ld_in(b + loff + LT::S * (BHAT ? brv5(j) : (uint32_t)j));
@@ -673,7 +682,7 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
             fwd_pass2<P>(rb, ftw2 + opaque_zero(), L.lane);
         }
 #pragma unroll
-        for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(ra[j], umin(rb[j], rb[j] - P::Q2));   // b-hat < 2q
+        for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(ra[j], csub<P::Q2>(rb[j]));   // b-hat < 2q
         inv_pass2<P>(ra, itw2 + opaque_zero(), L.lane);
         lds_p2_to_p1<P>(ra, buf, L);
         uint32_t *pc = c + off;
@@ -696,9 +705,9 @@ __global__ __launch_bounds__(WG) void k_pointwise(const uint4 *a, const uint4 *b
         uint32_t v[4] = {x.x, x.y, x.z, x.w}, w[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            uint32_t m = mont_mul<P>(umin(v[k], v[k] - P::Q2), umin(w[k], w[k] - P::Q2));
+            uint32_t m = mont_mul<P>(csub<P::Q2>(v[k]), csub<P::Q2>(w[k]));
             m = shoup_mul<P::Q>(m, P::R, RP);
-            v[k] = umin(m, m - P::Q);
+            v[k] = csub<P::Q>(m);
         }
         c[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }

@@ -33,6 +33,30 @@ OP_KERNEL(k_mad_u24, "v_mad_u32_u24 %0, %0, %1, %1")
 OP_KERNEL(k_fma_f32, "v_fma_f32 %0, %0, %1, %1")
 OP_KERNEL(k_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
 OP_KERNEL(k_perm, "v_perm_b32 %0, %0, %1, %1")
+OP_KERNEL(k_sub, "v_sub_u32 %0, %0, %1")
+OP_KERNEL(k_max, "v_max_u32 %0, %0, %1")
+OP_KERNEL(k_med3, "v_med3_u32 %0, %0, %1, %1")
+OP_KERNEL(k_and, "v_and_b32 %0, %0, %1")
+OP_KERNEL(k_xor, "v_xor_b32 %0, %0, %1")
+OP_KERNEL(k_lshl_add, "v_lshl_add_u32 %0, %0, 1, %1")
+OP_KERNEL(k_sub_e64, "v_sub_u32_e64 %0, %0, %1")
+OP_KERNEL(k_mul_hi_i32, "v_mul_hi_i32 %0, %0, %1")
+// two-instruction reductions x -> x mod 2q (the butterflies' lazy reduction),
+// timed per pair
+#define PAIR_KERNEL(NAME, ASM)                                                            \
+    __global__ __launch_bounds__(256) void NAME(unsigned *out, unsigned seed, int iters)  \
+    {                                                                                     \
+        unsigned a[8], t;                                                                 \
+        for (int k = 0; k < 8; k++) a[k] = (threadIdx.x ^ seed) + k;                      \
+        const unsigned b = seed | 1;                                                      \
+        for (int i = 0; i < iters; i++) {                                                 \
+            _Pragma("unroll") for (int k = 0; k < 8; k++)                                 \
+                asm volatile(ASM : "+v"(a[k]), "=&v"(t) : "v"(b) : "vcc");                \
+        }                                                                                 \
+        out[blockIdx.x * 256 + threadIdx.x] = a[0] ^ a[1] ^ a[2] ^ a[3] ^ a[4] ^ a[5] ^ a[6] ^ a[7]; \
+    }
+PAIR_KERNEL(k_red_min, "v_sub_u32 %1, %0, %2\n\tv_min_u32 %0, %0, %1")
+PAIR_KERNEL(k_red_cnd, "v_sub_co_u32 %1, vcc, %0, %2\n\tv_cndmask_b32 %0, %1, %0, vcc")
 
 __global__ __launch_bounds__(256) void k_fma64(unsigned *out, unsigned seed, int iters)
 {
@@ -84,7 +108,10 @@ int main()
     unsigned *out;
     hipMalloc(&out, blocks * 256 * 4);
     struct K { const char *name; void (*fn)(unsigned *, unsigned, int); };
-    K ks[] = {{"v_add_u32", k_add}, {"v_min_u32", k_min}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_hi_u32", k_mul_hi},
+    K ks[] = {{"v_sub_u32", k_sub}, {"v_max_u32", k_max}, {"v_med3_u32", k_med3}, {"v_and_b32", k_and},
+              {"v_xor_b32", k_xor}, {"v_lshl_add_u32", k_lshl_add}, {"v_sub_u32_e64", k_sub_e64},
+              {"v_mul_hi_i32", k_mul_hi_i32}, {"sub+min (per pair)", k_red_min}, {"sub_co+cndmask (per pair)", k_red_cnd},
+              {"v_add_u32", k_add}, {"v_min_u32", k_min}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_hi_u32", k_mul_hi},
               {"v_mul_u32_u24", k_mul_u24}, {"v_mul_hi_u32_u24", k_mulhi_u24}, {"v_mad_u64_u32", k_mad64},
               {"v_add3_u32", k_add3}, {"v_mad_u32_u24", k_mad_u24}, {"v_fma_f32", k_fma_f32},
               {"v_cndmask_b32", k_cndmask}, {"v_perm_b32", k_perm}, {"v_fma_f64", k_fma64}, {"v_pk_add_u16", k_pk_add}};
