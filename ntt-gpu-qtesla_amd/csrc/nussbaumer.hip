@@ -4,25 +4,43 @@
 // equals poly_mul's bit for bit).  No roots of unity in the coefficient ring:
 // every "twiddle" is a negacyclic rotation of an inner polynomial.
 //
-// Geometry (one wave = one n=2048 product, or two n=1024 products):
+// Geometry: a PAIR of waves computes one n=2048 product (or two n=1024
+// products, one per 32-lane half); wave w of the pair owns half w of the
+// work at every level, so a lane never holds more than one half:
 //   outer level  (m = 32, as NTT.cu:193-201): 64 sub-polynomials of length
-//                R = n/32 in Z[y]/(y^R+1).  Lane a (a < R; R = 32 -> one product
-//                per 32-lane half) holds coefficient a of every sub-polynomial,
-//                register k holds sub-polynomial k.  Butterfly twiddles y^sr are
-//                lane rotations: one ds_bpermute + a per-lane sign fix.
-//   transpose    wave-private 32 KiB LDS, XOR-swizzled (conflict-free b32 on one
-//                side, b128 on the other; tests/test_nussbaumer_model.py).
-//   inner level  lane k owns sub-polynomial k of X and Y and multiplies them
-//                mod y^R+1 with a second Nussbaumer level (m' = R/8, r' = 8)
-//                entirely in registers: rotations are compile-time register
-//                renames, 2m' length-8 schoolbook products.  The 2m' points
-//                split into two independent blocks after the implicit first
-//                stage, which bounds the register peak at 3R values.
+//                R = n/32 in Z[y]/(y^R+1).  Lane a holds coefficient a of every
+//                sub-polynomial; wave w holds sub-polynomials 32w..32w+31 in
+//                registers.  The implicit first stage copies sub-polynomial k
+//                to k+32, so both waves start from the same 32 input words and
+//                the forward stages j = 4..0 never cross halves.  Butterfly
+//                twiddles y^sr are lane rotations: ds_bpermute + a sign fix.
+//   transposes   the pair's 32 KiB of LDS holds the X and Y matrices
+//                (XOR-swizzled rows, conflict-free b32 on one side, b128 on
+//                the other); each wave writes its half of both.
+//   inner level  lane k of wave w multiplies block w of X_k * Y_k mod y^R+1:
+//                a second Nussbaumer level (m' = R/8, r' = 8) in registers
+//                whose 2m' points split into two independent blocks after the
+//                implicit first stage; rotations are compile-time register
+//                renames, m' length-8 schoolbook products per block.  The two
+//                blocks meet again through LDS (last inner stage and the
+//                recombination of the halves, read back in the outer layout).
+//   outer inverse stages j = 0..4 per half; stage 5 and the final
+//                recombination (NTT.cu:272-277) exchange half a sub-polynomial
+//                set through LDS, each wave storing half of the output words.
+//   16 KiB of LDS and <= 256 VGPRs per wave -> 8 waves (2 per SIMD) per CU.
 //   deferred     the reference halves after every inverse butterfly (moddiv2,
 //   scaling      NTT.cu:255-258); here all 2^-L is applied once to `a` on load:
 //                a 32-bit rotate in Z/(2^32-1) (2^32 == 1), a Shoup multiply
 //                by 2^(32-L) mod q in Z/q (the 2^32 cancels the Montgomery REDC
 //                of the inner products).
+//
+// Z/q arithmetic is signed and lazy: values are int32 residues congruent mod q
+// with a compile-time magnitude bound; an add or sub is ONE instruction, and a
+// centred Barrett reduction (two instructions, |r| < ~q/2) runs on a whole
+// stage only where the bound would otherwise pass 2^31 (bounds tracked at
+// compile time in units of q/1024, see Ring<NTT_RING_Q> and Schedule).  The
+// inner products accumulate signed 64-bit (v_mad_i64_i32) and end in a signed
+// Montgomery REDC.  Z/(2^32-1) keeps the reference's ones'-complement words.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -35,9 +53,17 @@
 namespace qntt {
 namespace {
 
-constexpr int NUS_WG = 256;                     // 4 waves, one per SIMD
+#ifndef NUS_WG_CFG
+#define NUS_WG_CFG 512
+#endif
+#ifndef NUS_OCC_CFG
+#define NUS_OCC_CFG 2
+#endif
+constexpr int NUS_WG = NUS_WG_CFG;              // 8 waves = 4 pairs, two waves per SIMD
 constexpr int NUS_WAVES = NUS_WG / 64;
-constexpr int NUS_WAVE_WORDS = 8192;            // X and Y: 64 rows x R x H = 4096 words each
+constexpr int NUS_PAIRS = NUS_WAVES / 2;
+constexpr int NUS_MAT_WORDS = 4096;             // one 64-row x R x H matrix (16 KiB)
+constexpr int NUS_PAIR_WORDS = 2 * NUS_MAT_WORDS;
 constexpr int NUS_PPW_MAX = 16;
 
 template <int B, int E, class F>
@@ -58,10 +84,13 @@ __host__ __device__ constexpr int cbrv(int x, int bits)
 
 __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
-// LDS operations of one wave complete in issue order, so the wave-private
-// transposes need no s_barrier; this only keeps the compiler from moving
-// accesses across the phase boundaries
-__device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
+// LDS hand-offs between the two waves of a pair: a workgroup barrier (every
+// pair runs the same sequence, so all waves of the workgroup meet there)
+__device__ __forceinline__ void pair_sync() { __syncthreads(); }
+
+// keeps the compiler from hoisting the next LDS reads above this point (the
+// register peak of the inner level is the operand rows in flight)
+__device__ __forceinline__ void lds_order_fence() { asm volatile("" ::: "memory"); }
 
 __device__ __forceinline__ uint32_t bperm(uint32_t byte_addr, uint32_t v)
 {
@@ -93,12 +122,17 @@ __host__ __device__ constexpr uint32_t swz(uint32_t k)
 // ------------------------------------------------------------------------
 // rings
 // ------------------------------------------------------------------------
+// Both rings carry 32-bit words.  Bounds (Z/q only) are magnitudes in units
+// of q/1024, rounded up: RB after red(), IN after in_a / in_b, HR the largest
+// bound that stays below 2^31.  An add/sub of two values of bound B gives 2B.
 template <int RING, class P> struct Ring;
 
 // Z/(2^32-1): ones'-complement arithmetic (NTT.cu:102-134).  Values are any
-// 32-bit word; 0xFFFFFFFF is a second zero, mapped to 0 on output.
+// 32-bit word; 0xFFFFFFFF is a second zero, mapped to 0 on output.  Closed
+// under add/sub: no reductions (all bounds 0).
 template <class P>
 struct Ring<NTT_RING_M32, P> {
+    static constexpr int RB = 0, IN = 0, HR = 1 << 20;
     static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b)
     {
         uint32_t t;
@@ -112,10 +146,14 @@ struct Ring<NTT_RING_M32, P> {
         return t - (uint32_t)c;
     }
     static __device__ __forceinline__ uint32_t negm(uint32_t a, uint32_t m) { return a ^ m; }
+    static __device__ __forceinline__ uint32_t red(uint32_t a) { return a; }
     template <int L>
     static __device__ __forceinline__ uint32_t in_a(uint32_t x) { return __builtin_rotateright32(x, L); }
     static __device__ __forceinline__ uint32_t in_b(uint32_t x) { return x; }
+    template <int B>
     static __device__ __forceinline__ uint32_t out(uint32_t x) { return x == 0xFFFFFFFFu ? 0u : x; }
+    static constexpr bool mul_ok(int, int) { return true; }
+    static constexpr int mul_out(int, int) { return 0; }
     // negacyclic length-8 product; the 64-bit accumulator is folded after every
     // multiply-add (2^32 == 1) so it stays below 2^33 and never overflows
     static __device__ __forceinline__ void mul8(uint32_t (&z)[8], const uint32_t (&u)[8], const uint32_t (&v)[8])
@@ -137,66 +175,106 @@ struct Ring<NTT_RING_M32, P> {
     }
 };
 
-// Z/q: values kept in [0, q] (q itself is a second zero), canonical on output.
+// Z/q, signed lazy residues (file header).  red() is a centred Barrett with
+// MB = round(2^32 / q): e = round(a MB / 2^32) (one v_mad_i64_i32 with the
+// rounding constant), r = a - e q (one v_mad_u64_u32);
+// |a/q - a MB/2^32| < EPS for |a| < 2^31, so |r| < (1/2 + EPS) q.
 template <class P>
 struct Ring<NTT_RING_Q, P> {
     static constexpr uint32_t Q = P::Q;
-    static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b)
+    static constexpr int64_t MB = ((1ll << 32) + Q / 2) / Q;
+    static constexpr double EPS =
+        2147483648.0 * (double)((1ll << 32) > MB * Q ? (1ll << 32) - MB * Q : MB * Q - (1ll << 32)) /
+        ((double)Q * 4294967296.0);
+    static constexpr int RB = (int)((0.5 + EPS) * 1024.0) + 2;
+    static constexpr int IN = 1024;                                   // |x - q| <= q
+    static constexpr int HR = (int)(2147483647.0 / (double)Q * 1024.0) - 1;
+    static_assert(2 * RB <= HR, "a reduced value must survive one add/sub");
+
+    static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return a + b; }
+    static __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b) { return a - b; }
+    static __device__ __forceinline__ uint32_t negm(uint32_t a, uint32_t m) { return (a ^ m) - m; }
+    static __device__ __forceinline__ uint32_t red(uint32_t a)
     {
-        const uint32_t s = a + b;
-        return umin32(s, s - Q);
+        const uint32_t e = (uint32_t)(((int64_t)(int32_t)a * MB + 0x80000000ll) >> 32);
+        return (uint32_t)((uint64_t)e * (0u - Q) + a);
     }
-    static __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b)
-    {
-        const uint32_t d = a + Q - b;
-        return umin32(d, d - Q);
-    }
-    static __device__ __forceinline__ uint32_t negm(uint32_t a, uint32_t m) { return (m & (Q - a)) | (~m & a); }
     template <int L>
     static __device__ __forceinline__ uint32_t in_a(uint32_t x)
     {
-        // x * 2^(32-L) mod q (Shoup), [0, 2q) -> [0, q)
+        // x * 2^(32-L) mod q (Shoup), x < 2q -> [0, 2q) -> centred [-q, q)
         constexpr uint32_t S = (uint32_t)((uint64_t)cpow(2, 32 - L, Q) % Q);
         constexpr uint32_t SP = cshoup(S, Q);
         const uint32_t t = (uint32_t)((uint64_t)__umulhi(x, SP) * (0u - Q) + x * S);
-        return umin32(t, t - Q);
+        return t - Q;
     }
-    static __device__ __forceinline__ uint32_t in_b(uint32_t x) { return umin32(x, x - Q); }   // x < 2q
-    static __device__ __forceinline__ uint32_t out(uint32_t x) { return umin32(x, x - Q); }
-    // sum of 8 products <= 8 q^2 < 2^63, then one Montgomery REDC (x 2^-32)
+    static __device__ __forceinline__ uint32_t in_b(uint32_t x) { return x - Q; }   // x < 2q
+    // canonical [0, q) from a value of bound B
+    template <int B>
+    static __device__ __forceinline__ uint32_t out(uint32_t x)
+    {
+        if constexpr (B > RB) x = red(x);
+        return umin32(x, x + Q);   // (-q, q) -> [0, q)
+    }
+    // products of bounds Bu, Bv: 8 terms must fit a signed 64-bit accumulator
+    static constexpr bool mul_ok(int bu, int bv)
+    {
+        return 8.0 * (bu / 1024.0) * (bv / 1024.0) * (double)Q * (double)Q < 9.2e18;
+    }
+    // REDC output bound: |acc| / 2^32 + q/2
+    static constexpr int mul_out(int bu, int bv)
+    {
+        return (int)((8.0 * (bu / 1024.0) * (bv / 1024.0) * (double)Q / 4294967296.0 + 0.5) * 1024.0) + 2;
+    }
+    // negacyclic length-8 product, signed 64-bit sums, one signed Montgomery
+    // REDC per output (x 2^-32): m = acc * q^-1 mod 2^32, (acc - m q) / 2^32
     static __device__ __forceinline__ void mul8(uint32_t (&z)[8], const uint32_t (&u)[8], const uint32_t (&v)[8])
     {
-        static_assert((unsigned __int128)8 * Q * Q + (((unsigned __int128)Q) << 32) < ((unsigned __int128)1 << 64),
-                      "REDC input must fit 64 bits");
-        constexpr uint64_t TMAX = (uint64_t)(((unsigned __int128)8 * Q * Q) >> 32) + Q + 1;   // REDC output bound
-        static_assert(TMAX <= 3ull * Q, "at most two conditional subtractions");
         uint32_t vn[8];
 #pragma unroll
-        for (int j = 1; j < 8; ++j) vn[j] = Q - v[j];
+        for (int j = 1; j < 8; ++j) vn[j] = 0u - v[j];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            uint64_t acc = 0;
+            int64_t acc = 0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) acc += (uint64_t)u[j] * (j <= c ? v[c - j] : vn[8 + c - j]);
-            const uint32_t m = (uint32_t)acc * P::QNEG;
-            uint32_t t = (uint32_t)(((uint64_t)m * Q + acc) >> 32);
-            if constexpr (TMAX > 2ull * Q) t = umin32(t, t - 2 * Q);
-            z[c] = umin32(t, t - Q);
+            for (int j = 0; j < 8; ++j) acc += (int64_t)(int32_t)u[j] * (int32_t)(j <= c ? v[c - j] : vn[8 + c - j]);
+            const uint32_t m = (uint32_t)acc * (0u - P::QNEG);   // q^-1 mod 2^32
+            z[c] = (uint32_t)(acc >> 32) - (uint32_t)__mulhi((int)m, (int)Q);
         }
     }
 };
 
+// Bound bookkeeping of a transform stage: inputs of bound b are reduced
+// first when one add/sub would pass HR.
+template <class RG> constexpr bool stage_red(int b) { return 2 * b > RG::HR; }
+template <class RG> constexpr int stage_out(int b) { return 2 * (stage_red<RG>(b) ? RG::RB : b); }
+template <class RG> constexpr int stages_out(int b, int s) { return s == 0 ? b : stages_out<RG>(stage_out<RG>(b), s - 1); }
+template <class RG> constexpr int reduced_if(bool c, int b) { return c ? RG::RB : b; }
+
+template <class RG, int NREG>
+__device__ __forceinline__ void red_all(uint32_t (&v)[NREG])
+{
+#pragma unroll
+    for (int k = 0; k < NREG; ++k) v[k] = RG::red(v[k]);
+}
+
 // ------------------------------------------------------------------------
-// outer level (lane = coefficient, register = sub-polynomial)
+// outer level (lane = coefficient, register = sub-polynomial of half W)
 // ------------------------------------------------------------------------
-// forward, NTT.cu:203-244 with sr scaled by r/m; X and Y share the lane
-// addresses of each (stage, i) group
-template <class RG, class G>
-__device__ __forceinline__ void outer_fwd(uint32_t (&X)[64], uint32_t (&Y)[64], uint32_t a4, uint32_t hb4)
+// forward, NTT.cu:203-244 with sr scaled by r/m, stages j = 4..0 restricted to
+// the groups of half W (register k = sub-polynomial 32W + k); X and Y share
+// the lane addresses of each (stage, i) group.  Inputs of bound B0.
+template <class RG, class G, int B0, int W>
+__device__ __forceinline__ void outer_fwd_half(uint32_t (&X)[32], uint32_t (&Y)[32], uint32_t a4, uint32_t hb4)
 {
     static_for<0, 5>([&](auto JJ) {
-        constexpr int j = 4 - decltype(JJ)::value;
-        static_for<0, (1 << (5 - j))>([&](auto II) {
+        constexpr int s = decltype(JJ)::value, j = 4 - s;
+        if constexpr (stage_red<RG>(stages_out<RG>(B0, s))) {
+            red_all<RG>(X);
+            red_all<RG>(Y);
+        }
+        constexpr int gh = 1 << (4 - j);   // groups per half
+        static_for<W * gh, (W + 1) * gh>([&](auto II) {
             constexpr int i = decltype(II)::value;
             constexpr int sr = G::SC * (cbrv(i, 5 - j) << j);
             uint32_t addr = 0, mask = 0;
@@ -206,7 +284,7 @@ __device__ __forceinline__ void outer_fwd(uint32_t (&X)[64], uint32_t (&Y)[64], 
                 mask = (uint32_t)(d >> 31);
             }
             static_for<0, (1 << j)>([&](auto TT) {
-                constexpr int I = (i << (j + 1)) + decltype(TT)::value, L = I + (1 << j);
+                constexpr int I = (i << (j + 1)) + decltype(TT)::value - 32 * W, L = I + (1 << j);
                 uint32_t tx = X[L], ty = Y[L];
                 if constexpr (sr != 0) {
                     tx = RG::negm(bperm(addr, tx), mask);
@@ -221,15 +299,19 @@ __device__ __forceinline__ void outer_fwd(uint32_t (&X)[64], uint32_t (&Y)[64], 
     });
 }
 
-// inverse, NTT.cu:248-270 without the per-stage halving (deferred)
-template <class RG, class G>
-__device__ __forceinline__ void outer_inv(uint32_t (&Z)[64], uint32_t a4, uint32_t hb4)
+// inverse, NTT.cu:248-270 without the per-stage halving (deferred), stages
+// j = 0..4 of half W (stage 5 crosses the halves: see the kernel).  Inputs of
+// bound B0.
+template <class RG, class G, int B0, int W>
+__device__ __forceinline__ void outer_inv_half(uint32_t (&Z)[32], uint32_t a4, uint32_t hb4)
 {
-    static_for<0, 6>([&](auto JJ) {
+    static_for<0, 5>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
-        static_for<0, (1 << (5 - j))>([&](auto II) {
+        if constexpr (stage_red<RG>(stages_out<RG>(B0, j))) red_all<RG>(Z);
+        constexpr int gh = 1 << (4 - j);
+        static_for<W * gh, (W + 1) * gh>([&](auto II) {
             constexpr int i = decltype(II)::value;
-            constexpr int sr = j == 5 ? 0 : G::SC * (cbrv(i, 5 - j) << j);
+            constexpr int sr = G::SC * (cbrv(i, 5 - j) << j);
             uint32_t addr = 0, mask = 0;
             if constexpr (sr != 0) {
                 const int s = (int)a4 + 4 * sr;   // source lane a + sr; wraps (negated) when a + sr >= R
@@ -237,7 +319,7 @@ __device__ __forceinline__ void outer_inv(uint32_t (&Z)[64], uint32_t a4, uint32
                 mask = ~(uint32_t)((s - 4 * G::R) >> 31);
             }
             static_for<0, (1 << j)>([&](auto TT) {
-                constexpr int A = (i << (j + 1)) + decltype(TT)::value, B = A + (1 << j);
+                constexpr int A = (i << (j + 1)) + decltype(TT)::value - 32 * W, B = A + (1 << j);
                 const uint32_t t = RG::sub(Z[A], Z[B]);
                 Z[A] = RG::add(Z[A], Z[B]);
                 Z[B] = sr != 0 ? RG::negm(bperm(addr, t), mask) : t;
@@ -249,11 +331,13 @@ __device__ __forceinline__ void outer_inv(uint32_t (&Z)[64], uint32_t a4, uint32
 // ------------------------------------------------------------------------
 // inner level (lane = sub-polynomial; U[i'][j'] = coefficient MI*j' + i')
 // ------------------------------------------------------------------------
-template <class RG, class G, int BL>
+template <class RG, class G, int BL, int B0>
 __device__ __forceinline__ void inner_fwd_block(uint32_t (&U)[G::MI][8])
 {
     static_for<0, G::LMI>([&](auto JJ) {
-        constexpr int j = G::LMI - 1 - decltype(JJ)::value;
+        constexpr int s = decltype(JJ)::value, j = G::LMI - 1 - s;
+        if constexpr (stage_red<RG>(stages_out<RG>(B0, s)))
+            static_for<0, G::MI>([&](auto K) { red_all<RG>(U[decltype(K)::value]); });
         constexpr int cnt = 1 << (G::LMI - 1 - j);
         static_for<BL * cnt, (BL + 1) * cnt>([&](auto II) {
             constexpr int i = decltype(II)::value;
@@ -281,11 +365,13 @@ __device__ __forceinline__ void inner_fwd_block(uint32_t (&U)[G::MI][8])
     });
 }
 
-template <class RG, class G, int BL>
+template <class RG, class G, int BL, int B0>
 __device__ __forceinline__ void inner_inv_block(uint32_t (&Z)[G::MI][8])
 {
     static_for<0, G::LMI>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
+        if constexpr (stage_red<RG>(stages_out<RG>(B0, j)))
+            static_for<0, G::MI>([&](auto K) { red_all<RG>(Z[decltype(K)::value]); });
         constexpr int cnt = 1 << (G::LMI - 1 - j);
         static_for<BL * cnt, (BL + 1) * cnt>([&](auto II) {
             constexpr int i = decltype(II)::value;
@@ -310,95 +396,113 @@ __device__ __forceinline__ void inner_inv_block(uint32_t (&Z)[G::MI][8])
     });
 }
 
-// one inner block: rows -> forward block BL of X and Y -> 8-point products ->
-// inverse stages inside the block
-template <class RG, class G, int BL>
-__device__ __forceinline__ void inner_block(uint32_t (&Z)[G::MI][8], const uint32_t *xrow, const uint32_t *yrow,
-                                            uint32_t sw)
+// Bounds through the inner level for rows of bound BR: the forward's output,
+// a reduction if the products' accumulator needs it, the REDC output and the
+// inverse's output.
+template <class RG, class G, int BR> struct InnerBounds {
+    static constexpr int FWD = stages_out<RG>(BR, G::LMI);
+    static constexpr bool MRED = !RG::mul_ok(FWD, FWD);
+    static constexpr int MIN = reduced_if<RG>(MRED, FWD);
+    static_assert(RG::mul_ok(MIN, MIN), "inner products must fit the accumulator");
+    static constexpr int PROD = RG::mul_out(MIN, MIN);
+    static constexpr int INV = stages_out<RG>(PROD, G::LMI);
+};
+
+template <class G>
+__device__ __forceinline__ void read_row(uint32_t (&U)[G::MI][8], const uint32_t *row, uint32_t sw)
 {
-    uint32_t U[G::MI][8], V[G::MI][8];
 #pragma unroll
     for (int ch = 0; ch < G::R / 4; ++ch) {
-        const uint4 x = *(const uint4 *)(xrow + (((uint32_t)ch ^ sw) << 2));
+        const uint4 x = *(const uint4 *)(row + (((uint32_t)ch ^ sw) << 2));
         const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) U[(4 * ch + e) % G::MI][(4 * ch + e) / G::MI] = xs[e];
     }
-    inner_fwd_block<RG, G, BL>(U);
-#pragma unroll
-    for (int ch = 0; ch < G::R / 4; ++ch) {
-        const uint4 y = *(const uint4 *)(yrow + (((uint32_t)ch ^ sw) << 2));
-        const uint32_t ys[4] = {y.x, y.y, y.z, y.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) V[(4 * ch + e) % G::MI][(4 * ch + e) / G::MI] = ys[e];
+}
+
+// block BL of one row product: rows of X and Y from LDS -> forward block BL
+// of both -> m' 8-point products -> inverse stages inside the block
+template <class RG, class G, int BL, int BR>
+__device__ __forceinline__ void inner_block(uint32_t (&Z)[G::MI][8], const uint32_t *xrow, const uint32_t *yrow,
+                                            uint32_t sw)
+{
+    using IB = InnerBounds<RG, G, BR>;
+    uint32_t U[G::MI][8], V[G::MI][8];
+    read_row<G>(U, xrow, sw);
+    inner_fwd_block<RG, G, BL, BR>(U);
+    lds_order_fence();
+    read_row<G>(V, yrow, sw);
+    inner_fwd_block<RG, G, BL, BR>(V);
+    if constexpr (IB::MRED) {
+        static_for<0, G::MI>([&](auto K) {
+            red_all<RG>(U[decltype(K)::value]);
+            red_all<RG>(V[decltype(K)::value]);
+        });
     }
-    inner_fwd_block<RG, G, BL>(V);
 #pragma unroll
     for (int i = 0; i < G::MI; ++i) RG::mul8(Z[i], U[i], V[i]);
-    inner_inv_block<RG, G, BL>(Z);
+    inner_inv_block<RG, G, BL, IB::PROD>(Z);
 }
 
-// lane k: W = X_k * Y_k * 2^(LMI+1) mod (y^R + 1), written back over the X row
-template <class RG, class G>
-__device__ __forceinline__ void inner_product(uint32_t *xrow, const uint32_t *yrow, uint32_t sw)
+// Bounds of the last inner stage (s = Z0 + Z1, d = Z0 - Z1) and of the
+// recombination W[c] = s[c] + d[c - m'] (negated when it wraps).
+template <class RG, class G, int BR> struct RowOutBounds {
+    static constexpr int INV = InnerBounds<RG, G, BR>::INV;
+    static constexpr bool R1 = stage_red<RG>(INV);
+    static constexpr int REC = stage_out<RG>(INV);
+    static constexpr bool R2 = stage_red<RG>(REC);
+    static constexpr int W = stage_out<RG>(REC);
+};
+
+// Whole-product bound schedule (units of q/1024; 0 everywhere for Z/(2^32-1)).
+template <class RG> struct Schedule {
+    static constexpr int OFWD = stages_out<RG>(RG::IN, 5);   // after the outer forward
+    // rows enter the inner level reduced when the forward left them above RB
+    static constexpr bool ROWRED = OFWD > RG::RB;
+    static constexpr int ROW = reduced_if<RG>(ROWRED, OFWD);
+};
+
+// offset of coefficient a of row (h, k) inside a matrix
+template <int R>
+__device__ __forceinline__ uint32_t mat_off(uint32_t h, int k, uint32_t a)
 {
-    uint32_t Z0[G::MI][8], Z1[G::MI][8];
-    inner_block<RG, G, 0>(Z0, xrow, yrow, sw);
-    inner_block<RG, G, 1>(Z1, xrow, yrow, sw);
-    uint32_t W[G::R];
-#pragma unroll
-    for (int t = 0; t < G::MI; ++t) {   // last inverse stage (j = LMI, sr = 0) + recombination
-#pragma unroll
-        for (int a = 0; a < 8; ++a) {
-            const uint32_t s = RG::add(Z0[t][a], Z1[t][a]), d = RG::sub(Z0[t][a], Z1[t][a]);
-            Z0[t][a] = s;
-            Z1[t][a] = d;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < G::MI; ++i) {
-        W[i] = RG::sub(Z0[i][0], Z1[i][7]);
-#pragma unroll
-        for (int j = 1; j < 8; ++j) W[G::MI * j + i] = RG::add(Z0[i][j], Z1[i][j - 1]);
-    }
-    wave_lds_fence();
-#pragma unroll
-    for (int ch = 0; ch < G::R / 4; ++ch)
-        *(uint4 *)(xrow + (((uint32_t)ch ^ sw) << 2)) = make_uint4(W[4 * ch], W[4 * ch + 1], W[4 * ch + 2], W[4 * ch + 3]);
+    return (h * 64 + k) * R + (a ^ (swz<R>(k) << 2));
 }
 
-template <int PS, int RING>
-__global__ __launch_bounds__(NUS_WG, 1) void k_nussbaumer(const uint32_t *a, const uint32_t *b, uint32_t *c,
-                                                         uint32_t npoly, uint32_t ppw)
+// One unit (one n=2048 product or two n=1024 products) by wave W of a pair.
+template <int PS, int RING, int W>
+__device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t u,
+                                         uint32_t *pl)
 {
     using P = typename PSel<PS>::T;
     using G = Geo<P::N>;
     using RG = Ring<RING, P>;
-    constexpr int R = G::R, H = G::H;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[NUS_WAVES * NUS_WAVE_WORDS];
+    using SCH = Schedule<RG>;
+    using OB = RowOutBounds<RG, G, SCH::ROW>;
+    constexpr int R = G::R, H = G::H, MI = G::MI;
+    uint32_t *const xm = pl, *const ym = pl + NUS_MAT_WORDS;
 
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t *const wl = lds + wave * NUS_WAVE_WORDS;
-    const uint32_t ca = lane & (R - 1), h = lane / R;        // outer layout
+    // lane, opaque per unit: the ~30 per-group rotation addresses and masks and
+    // the ~30 swizzled LDS offsets derived from it are recomputed (1-3 VALU
+    // each) instead of being hoisted out of the unit loop into registers
+    // (they would spill to scratch)
+    uint32_t lane = threadIdx.x & 63u;
+    asm volatile("" : "+v"(lane));
+    const uint32_t ca = lane & (R - 1), h = lane / R;   // outer layout
     const uint32_t a4 = ca * 4, hb4 = h * R * 4;
-    const uint32_t nunits = (npoly + H - 1) / H;
+    const uint32_t poly = u * H + h;
+    const bool valid = poly < npoly;
+    // loads are unconditional: an idle half-wave (odd n=1024 batch) reads the
+    // unit's first product and never stores; both waves of the pair load the
+    // same words (the implicit first stage copies sub-polynomial k to k + 32)
+    const size_t loff = (size_t)(valid ? poly : u * H) * P::N + 32u * ca;
 
-    uint32_t u = blockIdx.x * (NUS_WAVES * ppw) + wave;
-#pragma unroll 1
-    for (uint32_t it = 0; it < ppw; ++it, u += NUS_WAVES) {
-        if (u >= nunits) break;
-        const uint32_t poly = u * H + h;
-        const bool valid = poly < npoly;
-        const size_t off = (size_t)poly * P::N + 32u * ca;
-
-        uint32_t X[64], Y[64];
+    {
+        uint32_t X[32], Y[32];
 #pragma unroll
         for (int q4 = 0; q4 < 8; ++q4) {
-            uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
-            if (valid) {
-                x = *(const uint4 *)(a + off + 4 * q4);
-                y = *(const uint4 *)(b + off + 4 * q4);
-            }
+            const uint4 x = *(const uint4 *)(a + loff + 4 * q4);
+            const uint4 y = *(const uint4 *)(b + loff + 4 * q4);
             X[4 * q4 + 0] = RG::template in_a<G::L>(x.x);
             X[4 * q4 + 1] = RG::template in_a<G::L>(x.y);
             X[4 * q4 + 2] = RG::template in_a<G::L>(x.z);
@@ -408,44 +512,135 @@ __global__ __launch_bounds__(NUS_WG, 1) void k_nussbaumer(const uint32_t *a, con
             Y[4 * q4 + 2] = RG::in_b(y.z);
             Y[4 * q4 + 3] = RG::in_b(y.w);
         }
-#pragma unroll
-        for (int k = 0; k < 32; ++k) {   // implicit first stage: X1[i + 32] = X1[i] (NTT.cu:196-200)
-            X[k + 32] = X[k];
-            Y[k + 32] = Y[k];
+        outer_fwd_half<RG, G, RG::IN, W>(X, Y, a4, hb4);
+        if constexpr (SCH::ROWRED) {
+            red_all<RG>(X);
+            red_all<RG>(Y);
         }
-        outer_fwd<RG, G>(X, Y, a4, hb4);
+        // this half's rows of both matrices
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            xm[mat_off<R>(h, 32 * W + k, ca)] = X[k];
+            ym[mat_off<R>(h, 32 * W + k, ca)] = Y[k];
+        }
+    }
+    pair_sync();
 
-        // transpose: row (h, k) of X at wl[(h*64 + k)*R ...], Y at +4096
-        wave_lds_fence();
+    // block W of every row product: lane = sub-polynomial (row), all H products
+    uint32_t Zb[H][MI][8];
 #pragma unroll
-        for (int k = 0; k < 64; ++k) {
-            const uint32_t o = (h * 64 + k) * R + (ca ^ (swz<R>(k) << 2));
-            wl[o] = X[k];
-            wl[4096 + o] = Y[k];
+    for (int hh = 0; hh < H; ++hh)
+        inner_block<RG, G, W, SCH::ROW>(Zb[hh], xm + (hh * 64 + lane) * R, ym + (hh * 64 + lane) * R, swz<R>(lane));
+    pair_sync();   // both waves are done reading the matrices
+    uint32_t *const zm = W == 0 ? xm : ym;   // block W's results, same row layout
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) {
+        uint32_t *row = zm + (hh * 64 + lane) * R;
+#pragma unroll
+        for (int ch = 0; ch < R / 4; ++ch) {
+            const int c0 = 4 * ch;
+            *(uint4 *)(row + (((uint32_t)ch ^ swz<R>(lane)) << 2)) =
+                make_uint4(Zb[hh][(c0 + 0) % MI][(c0 + 0) / MI], Zb[hh][(c0 + 1) % MI][(c0 + 1) / MI],
+                           Zb[hh][(c0 + 2) % MI][(c0 + 2) / MI], Zb[hh][(c0 + 3) % MI][(c0 + 3) / MI]);
         }
-        wave_lds_fence();
-#pragma unroll
-        for (int hh = 0; hh < H; ++hh) {
-            uint32_t *xrow = wl + (hh * 64 + lane) * R;
-            inner_product<RG, G>(xrow, xrow + 4096, swz<R>(lane));
-        }
-        wave_lds_fence();
-        uint32_t Z[64];
-#pragma unroll
-        for (int k = 0; k < 64; ++k) Z[k] = wl[(h * 64 + k) * R + (ca ^ (swz<R>(k) << 2))];
-        wave_lds_fence();
-        outer_inv<RG, G>(Z, a4, hb4);
+    }
+    pair_sync();
 
-        // recombination (NTT.cu:272-277): c[32a + i] = Z_i[a] + Z_{32+i}[a-1], wrapping negated
-        const uint32_t d1 = a4 - 4, addr1 = (d1 & (4u * R - 1)) | hb4, mask1 = (uint32_t)((int)d1 >> 31);
-        uint32_t o[32];
+    // back in the outer layout for this half: the last inner stage of the two
+    // blocks (s, d) and the recombination W[a] = s[a] + d[a - m'], negated
+    // when it wraps (a < m')
+    uint32_t Z[32];
+    {
+        const uint32_t ap = (ca - MI) & (R - 1);
+        const uint32_t wmask = ca < (uint32_t)MI ? 0xFFFFFFFFu : 0u;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) o[i] = RG::out(RG::add(Z[i], RG::negm(bperm(addr1, Z[32 + i]), mask1)));
-        if (valid) {   // both halves of a lane group share validity, so bpermute sources are valid lanes
-#pragma unroll
-            for (int q4 = 0; q4 < 8; ++q4)
-                *(uint4 *)(c + off + 4 * q4) = make_uint4(o[4 * q4], o[4 * q4 + 1], o[4 * q4 + 2], o[4 * q4 + 3]);
+        for (int k = 0; k < 32; ++k) {
+            const int kk = 32 * W + k;
+            uint32_t z0 = xm[mat_off<R>(h, kk, ca)], z1 = ym[mat_off<R>(h, kk, ca)];
+            uint32_t p0 = xm[mat_off<R>(h, kk, ap)], p1 = ym[mat_off<R>(h, kk, ap)];
+            if constexpr (OB::R1) {
+                z0 = RG::red(z0);
+                z1 = RG::red(z1);
+                p0 = RG::red(p0);
+                p1 = RG::red(p1);
+            }
+            uint32_t s = RG::add(z0, z1), d = RG::sub(p0, p1);
+            if constexpr (OB::R2) {
+                s = RG::red(s);
+                d = RG::red(d);
+            }
+            Z[k] = RG::add(s, RG::negm(d, wmask));
         }
+    }
+    outer_inv_half<RG, G, OB::W, W>(Z, a4, hb4);
+    constexpr int B5 = stages_out<RG>(OB::W, 5);
+    pair_sync();   // both waves are done reading the block results
+
+    // stage 5 (sr = 0) pairs sub-polynomials i and i + 32 across the halves,
+    // then c[32a + i] = Z'_i[a] + Z'_{32+i}[a-1] (NTT.cu:272-277); wave W
+    // finishes i in [16W, 16W + 16) with the other wave's registers 16W..16W+15
+    {
+        uint32_t *xo = pl + W * 1024;   // what the other wave needs
+#pragma unroll
+        for (int k = 0; k < 16; ++k) xo[k * 64 + lane] = Z[16 * (1 - W) + k];
+    }
+    pair_sync();
+    const uint32_t *xi = pl + (1 - W) * 1024;
+    const uint32_t d1 = a4 - 4, addr1 = (d1 & (4u * R - 1)) | hb4, mask1 = (uint32_t)((int)d1 >> 31);
+    constexpr bool FR5 = stage_red<RG>(B5);
+    constexpr int BA = stage_out<RG>(B5);
+    constexpr bool FRO = stage_red<RG>(BA);
+    uint32_t o[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const int i = 16 * W + t;   // output column
+        // sub-polynomial i (half 0) and i + 32 (half 1)
+        uint32_t zl = W == 0 ? Z[i] : xi[t * 64 + lane];
+        uint32_t zh = W == 0 ? xi[t * 64 + lane] : Z[i];
+        if constexpr (FR5) {
+            zl = RG::red(zl);
+            zh = RG::red(zh);
+        }
+        uint32_t A = RG::add(zl, zh), B = RG::sub(zl, zh);
+        if constexpr (FRO) {
+            A = RG::red(A);
+            B = RG::red(B);
+        }
+        o[t] = RG::template out<stage_out<RG>(BA)>(RG::add(A, RG::negm(bperm(addr1, B), mask1)));
+    }
+    if (valid) {   // both halves of a lane group share validity, so bpermute sources are valid lanes
+        uint32_t *dst = c + (size_t)poly * P::N + 32u * ca + 16 * W;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4)
+            *(uint4 *)(dst + 4 * q4) = make_uint4(o[4 * q4], o[4 * q4 + 1], o[4 * q4 + 2], o[4 * q4 + 3]);
+    }
+    pair_sync();   // the exchange area is free for the next unit
+}
+
+template <int PS, int RING>
+__global__ __launch_bounds__(NUS_WG, NUS_OCC_CFG) void k_nussbaumer(const uint32_t *a, const uint32_t *b, uint32_t *c,
+                                                                   uint32_t npoly, uint32_t ppw)
+{
+    using P = typename PSel<PS>::T;
+    constexpr int H = Geo<P::N>::H;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NUS_PAIRS * NUS_PAIR_WORDS];
+    const uint32_t wave = threadIdx.x >> 6, pair = wave >> 1;
+    uint32_t *const pl = lds + pair * NUS_PAIR_WORDS;
+    const uint32_t nunits = (npoly + H - 1) / H;
+    // every pair of the workgroup runs the same number of units (idle pairs
+    // past the batch still meet the barriers)
+    uint32_t u = blockIdx.x * (NUS_PAIRS * ppw) + pair;
+    const uint32_t first = blockIdx.x * (NUS_PAIRS * ppw);
+    if (first >= nunits) return;   // whole workgroup idle (uniform)
+    const uint32_t wg_units = min((uint32_t)(NUS_PAIRS * ppw), nunits - first);
+    const uint32_t steps = (wg_units + NUS_PAIRS - 1) / NUS_PAIRS;
+#pragma unroll 1
+    for (uint32_t it = 0; it < steps; ++it, u += NUS_PAIRS) {
+        // a pair past the batch recomputes the workgroup's first unit and stores nothing
+        const uint32_t uu = u < nunits ? u : first;
+        const uint32_t np = u < nunits ? npoly : 0u;
+        if ((wave & 1) == 0) nus_unit<PS, RING, 0>(a, b, c, np, uu, pl);
+        else nus_unit<PS, RING, 1>(a, b, c, np, uu, pl);
     }
 }
 
@@ -454,11 +649,11 @@ __global__ __launch_bounds__(NUS_WG, 1) void k_nussbaumer(const uint32_t *a, con
 int nussbaumer_launch(int ps, int ring, const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, void *stream,
                       int cus)
 {
-    const size_t per_wave = ps == 2 ? 1 : 2;
-    const size_t units = (batch + per_wave - 1) / per_wave;
-    size_t ppw = units / ((size_t)NUS_WAVES * (size_t)cus * 4);
+    const size_t per_unit = ps == 2 ? 1 : 2;
+    const size_t units = (batch + per_unit - 1) / per_unit;
+    size_t ppw = units / ((size_t)NUS_PAIRS * (size_t)cus * 2);
     ppw = ppw < 1 ? 1 : (ppw > NUS_PPW_MAX ? NUS_PPW_MAX : ppw);
-    const dim3 grid((uint32_t)((units + NUS_WAVES * ppw - 1) / (NUS_WAVES * ppw)));
+    const dim3 grid((uint32_t)((units + NUS_PAIRS * ppw - 1) / (NUS_PAIRS * ppw)));
     hipStream_t s = (hipStream_t)stream;
     const uint32_t nb = (uint32_t)batch, pw = (uint32_t)ppw;
 #define QNTT_NUS(PSV, RV)                                                                                   \

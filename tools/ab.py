@@ -41,6 +41,7 @@ def main():
             getattr(L, nm).argtypes = [vp, vp, sz, ctypes.c_int, vp]
         L.poly_mul.argtypes = [vp, vp, vp, sz, ctypes.c_int, vp]
         L.poly_mul_ntt.argtypes = [vp, vp, vp, sz, ctypes.c_int, vp]
+        L.poly_mul_nussbaumer.argtypes = [vp, vp, vp, sz, ctypes.c_int, ctypes.c_int, vp]
         libs[os.path.basename(path)] = L
     x = torch.empty(args.batch * n, dtype=torch.int32, device="cuda")
     y = torch.empty_like(x)
@@ -56,6 +57,9 @@ def main():
             rc = L.poly_ntt_oop(dst.data_ptr(), x.data_ptr(), args.batch, ps, s.cuda_stream)
         elif op == "inv":
             rc = L.poly_invntt_oop(dst.data_ptr(), x.data_ptr(), args.batch, ps, s.cuda_stream)
+        elif op in ("nus", "nusm32"):
+            rc = L.poly_mul_nussbaumer(z.data_ptr(), x.data_ptr(), y.data_ptr(), args.batch, ps, 1 if op == "nusm32" else 0,
+                                       s.cuda_stream)
         elif op == "mulntt":
             rc = L.poly_mul_ntt(z.data_ptr(), x.data_ptr(), y.data_ptr(), args.batch, ps, s.cuda_stream)
         else:
