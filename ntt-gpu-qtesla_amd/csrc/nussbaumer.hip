@@ -27,7 +27,8 @@
 //   outer inverse stages j = 0..4 per half; stage 5 and the final
 //                recombination (NTT.cu:272-277) exchange half a sub-polynomial
 //                set through LDS, each wave storing half of the output words.
-//   16 KiB of LDS and <= 256 VGPRs per wave -> 8 waves (2 per SIMD) per CU.
+//   16 KiB of LDS and <= 256 VGPRs per wave -> 8 waves (2 per SIMD) per CU,
+//   one pair per workgroup.
 //   deferred     the reference halves after every inverse butterfly (moddiv2,
 //   scaling      NTT.cu:255-258); here all 2^-L is applied once to `a` on load:
 //                a 32-bit rotate in Z/(2^32-1) (2^32 == 1), a Shoup multiply
@@ -54,12 +55,15 @@ namespace qntt {
 namespace {
 
 #ifndef NUS_WG_CFG
-#define NUS_WG_CFG 512
+#define NUS_WG_CFG 128   // one pair per workgroup: its barriers wait for the partner only
 #endif
 #ifndef NUS_OCC_CFG
 #define NUS_OCC_CFG 2
 #endif
-constexpr int NUS_WG = NUS_WG_CFG;              // 8 waves = 4 pairs, two waves per SIMD
+// one pair per workgroup (32 KiB LDS), 4 workgroups per CU at <= 256 VGPRs:
+// 2 waves per SIMD; 4 pairs per 512-thread workgroup measured 1.29x slower
+// (every barrier then waits for all 8 waves, profiles/r02/ab_nussbaumer_wg.log)
+constexpr int NUS_WG = NUS_WG_CFG;
 constexpr int NUS_WAVES = NUS_WG / 64;
 constexpr int NUS_PAIRS = NUS_WAVES / 2;
 constexpr int NUS_MAT_WORDS = 4096;             // one 64-row x R x H matrix (16 KiB)
@@ -84,8 +88,9 @@ __host__ __device__ constexpr int cbrv(int x, int bits)
 
 __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
-// LDS hand-offs between the two waves of a pair: a workgroup barrier (every
-// pair runs the same sequence, so all waves of the workgroup meet there)
+// LDS hand-offs between the two waves of a pair: a workgroup barrier (the
+// workgroup is one pair; with several pairs per workgroup every pair runs the
+// same sequence, so all waves meet there)
 __device__ __forceinline__ void pair_sync() { __syncthreads(); }
 
 // keeps the compiler from hoisting the next LDS reads above this point (the
