@@ -153,9 +153,13 @@ struct Lane {
     uint32_t rbase, rxm;   // pass-2 LDS read/write (b128) address parts
     uint32_t brl;          // lane index within its poly: pass-1 column, and bitrev(Lp)
 
-    __device__ __forceinline__ Lane()
+    __device__ __forceinline__ Lane() : Lane(threadIdx.x & 63) {}
+    // from a lane index the compiler cannot see through (opaque_lane): the
+    // derived LDS addresses are recomputed where they are used instead of
+    // being kept live across a whole work unit
+    __device__ __forceinline__ explicit Lane(uint32_t lane_)
     {
-        lane = threadIdx.x & 63;
+        lane = lane_;
         h = lane >> 5;
         // pass-2 row of this lane: Lp = bitrev(lane).  Then the bit-reversed
         // side of each transform (forward store, inverse load) addresses
@@ -167,6 +171,15 @@ struct Lane {
         rbase = 32 * (Lp ^ ((Lp >> 2) & 1)) + (BIG ? 0u : 1024 * h);
         brl = BIG ? lane : (lane & 31);
     }
+    // word offset of this lane's pass-1 column relative to the first word of
+    // unit u (a wave-uniform base, u * UPW * N): stores, and loads with the
+    // odd-batch rule of load_poly
+    __device__ __forceinline__ uint32_t col() const { return BIG ? brl : h * P::N + brl; }
+    __device__ __forceinline__ uint32_t col_load(uint32_t u, uint32_t npoly) const
+    {
+        return BIG ? brl : ((u * UPW + h < npoly) ? h * P::N : 0u) + brl;
+    }
+    __device__ __forceinline__ static size_t unit_base(uint32_t u) { return (size_t)u * (UPW * P::N); }
     // index of this lane's polynomial in wave unit u
     __device__ __forceinline__ uint32_t poly(uint32_t u) const { return u * UPW + (BIG ? 0u : h); }
     // the polynomial this lane loads from: its own, or for the second half of
@@ -220,6 +233,18 @@ __device__ __forceinline__ uint32_t opaque_zero()
     asm volatile("" : "+s"(z));
     return z;
 }
+
+__device__ __forceinline__ uint32_t opaque_lane()
+{
+    uint32_t l = threadIdx.x & 63;
+    asm volatile("" : "+v"(l));
+    return l;
+}
+
+// wave index within the workgroup, as a scalar (wave-uniform) value: unit
+// indices and per-unit base addresses derived from it stay in SGPRs, so the
+// global accesses take the saddr + 32-bit lane offset form
+__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 constexpr int XPOSE_WORDS = 2048;   // per-wave transpose buffer (8 KiB)
 
@@ -341,11 +366,13 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
     }
 }
 
-template <class P>
+// BMIN > 0 stops short: the stages on pos bits BMIN-1..0 are left out
+// (poly_mul's incomplete transform, basemul4)
+template <class P, int BMIN = 0>
 __device__ __forceinline__ void fwd_pass2(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
 {
 #pragma unroll
-    for (int b = 4; b >= 0; --b) {
+    for (int b = 4; b >= BMIN; --b) {
         const int hh = 1 << b;
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
@@ -358,11 +385,11 @@ __device__ __forceinline__ void fwd_pass2(uint32_t (&r)[32], const uint2 *tab, u
     }
 }
 
-template <class P>
+template <class P, int BMIN = 0>
 __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
 {
 #pragma unroll
-    for (int b = 0; b <= 4; ++b) {
+    for (int b = BMIN; b <= 4; ++b) {
         const int hh = 1 << b;
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
@@ -371,6 +398,50 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
                 const uint2 w = tab[e * 64 + lane];
                 gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
             }
+        }
+    }
+}
+
+// Products in the incomplete NTT domain of poly_mul: after the forward's
+// stages down to pos bit 2, register group g = j>>2 of a lane holds the
+// residue of its polynomial mod x^4 - zeta (coefficient i in register 4g+i),
+// zeta = +w for g even and -w for g odd, w = psi^brv(k) the twiddle of the
+// stage on pos bit 2 (LDS entry 3 + (g>>1)).  Per residue: a, b canonical,
+// b~_i = zeta b_i (negated Shoup product, two-candidate min), the four sums
+// of four products in 64 bits (< 4q^2) and one Montgomery REDC each,
+// (c + m q) / 2^32 with m = -c q^-1 mod 2^32 (one v_mad_u64_u32): output in
+// [0, 2q), times 2^-32 (folded into the final scaling, NINV4_R).  Replaces
+// the forward's last two stages on both operands, the inverse's first two
+// and the pointwise product: ~430 fewer VALU per unit.
+template <class P>
+__device__ __forceinline__ void basemul4(uint32_t (&ra)[32], const uint32_t (&rb)[32], const uint2 *tab, uint32_t lane)
+{
+    static_assert(4.0 * P::Q * (double)P::Q + 4294967296.0 * P::Q < 18446744073709551616.0, "REDC input fits 64 bits");
+    static_assert(4.0 * P::Q * (double)P::Q / 4294967296.0 + P::Q < 2.0 * P::Q, "REDC output below 2q");
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        const uint2 w = tab[(3 + (g >> 1)) * 64 + lane];   // (-w mod 2^32, w')
+        uint32_t a[4], b[4], bt[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a[i] = canon4<P>(ra[4 * g + i]);
+            b[i] = canon4<P>(rb[4 * g + i]);
+        }
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+            const uint32_t tn = madlo32(__umulhi(rb[4 * g + i], w.y), P::Q, rb[4 * g + i] * w.x);   // -(b w mod q), in (-2q, 0]
+            // zeta b_i as a value in [0, q]: +w -> min(-tn, -tn - q); -w -> min(tn + q, tn + 2q)
+            bt[i] = (g & 1) ? umin(tn + P::Q, tn + P::Q2) : umin(0u - tn, (0u - P::Q) - tn);
+        }
+        uint64_t c[4];
+        c[0] = (uint64_t)a[0] * b[0] + (uint64_t)a[1] * bt[3] + (uint64_t)a[2] * bt[2] + (uint64_t)a[3] * bt[1];
+        c[1] = (uint64_t)a[0] * b[1] + (uint64_t)a[1] * b[0] + (uint64_t)a[2] * bt[3] + (uint64_t)a[3] * bt[2];
+        c[2] = (uint64_t)a[0] * b[2] + (uint64_t)a[1] * b[1] + (uint64_t)a[2] * b[0] + (uint64_t)a[3] * bt[3];
+        c[3] = (uint64_t)a[0] * b[3] + (uint64_t)a[1] * b[2] + (uint64_t)a[2] * b[1] + (uint64_t)a[3] * b[0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t m = (uint32_t)c[i] * P::QNEG;
+            ra[4 * g + i] = (uint32_t)(((uint64_t)m * P::Q + c[i]) >> 32);
         }
     }
 }
@@ -460,7 +531,7 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
                                            Process &process)
 {
     uint32_t r[32];
-    uint32_t u = blockIdx.x * (WAVES * ppw) + (threadIdx.x >> 6);
+    uint32_t u = blockIdx.x * (WAVES * ppw) + wave_id();
     if (u < nunits) load(r, u);
     prologue();   // every wave reaches the barrier inside
     if (u >= nunits) return;
@@ -482,27 +553,22 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
 #ifndef NTT_WG
 #define NTT_WG 512   // fwd / inv: 8 waves, 64 + 15.75 KiB LDS -> 2 WG/CU
 #endif
-// poly_mul workgroup per parameter set: n=2048 runs 16 waves (128 + 31.5 KiB
-// LDS, 1 WG/CU, <=128 VGPRs -> 4 waves/SIMD); n=1024 keeps 8 waves at <=256
-// VGPRs (2 waves/SIMD; at 128 VGPRs it spills 60 and loses 37 %),
-// profiles/r01/ab_poly_mul_wg.json
+// poly_mul workgroup: 16 waves (128 + 31.5 KiB LDS, 1 WG/CU) at <= 128 VGPRs
+// -> 4 waves/SIMD for both n.  n=1024 ran 8 waves at 2 waves/SIMD before the
+// incomplete-domain product and the per-transpose address recomputation
+// (fresh lanes) brought it under 128 VGPRs: 4 waves/SIMD is 4 % faster there
+// (poly_mul_ntt 8 %), profiles/r02/ab_polymul_incomplete.log
 #ifndef MUL_WG
-#define MUL_WG 512
-#endif
-#ifndef MUL_WG_BIG
-#define MUL_WG_BIG 1024
+#define MUL_WG 1024
 #endif
 #ifndef NTT_WAVES_PER_SIMD
 #define NTT_WAVES_PER_SIMD 4
 #endif
 #ifndef MUL_WAVES_PER_SIMD
-#define MUL_WAVES_PER_SIMD 2
+#define MUL_WAVES_PER_SIMD 4
 #endif
-#ifndef MUL_WAVES_PER_SIMD_BIG
-#define MUL_WAVES_PER_SIMD_BIG 4
-#endif
-template <int PS> constexpr int mul_wg() { return PSel<PS>::T::LOGN == 11 ? MUL_WG_BIG : MUL_WG; }
-template <int PS> constexpr int mul_occ() { return PSel<PS>::T::LOGN == 11 ? MUL_WAVES_PER_SIMD_BIG : MUL_WAVES_PER_SIMD; }
+template <int PS> constexpr int mul_wg() { return MUL_WG; }
+template <int PS> constexpr int mul_occ() { return MUL_WAVES_PER_SIMD; }
 constexpr int WG = 256;   // elementwise kernels
 constexpr int NTT_WAVES = NTT_WG / 64;
 constexpr int NTT_LDS_WORDS = NTT_WAVES * XPOSE_WORDS + TW2_WORDS;
@@ -526,14 +592,14 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
 
     auto load = [&](uint32_t (&r)[32], uint32_t u) {   // pass-1 layout: natural lane index
-        load32(r, in + (size_t)L.load_poly(u, npoly) * P::N + L.brl, [](int j) { return LT::S * j; });
+        load32(r, in + LT::unit_base(u) + L.col_load(u, npoly), [](int j) { return LT::S * j; });
     };
     // canonical output: BR=false from the bit-reversed pass-2 registers to
     // natural order, brv5(j)*S + lane; BR=true from the pass-1 arrangement
     auto store = [&](uint32_t (&r)[32], uint32_t u) {
         const uint32_t poly = L.poly(u);
         if (LT::BIG || poly < npoly) {
-            uint32_t *dst = out + (size_t)poly * P::N + L.brl;
+            uint32_t *dst = out + LT::unit_base(u) + L.col();
             if constexpr (BR) dst += LT::BIG ? 32 * L.h : 0u;   // brl + 32 h = l5 + 64 h (p1s_off)
 #pragma unroll
             for (int j = 0; j < 32; ++j) st_out(dst + (BR ? p1s_off<P>(j) : brv5(j) * LT::S), canon4<P>(r[j]));
@@ -576,7 +642,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
     // BR=false: natural-order input; pass-2 position 32*Lp + j holds X[brv(pos)]
     // BR=true:  bit-reversed input read in the pass-1 arrangement, transposed below
     auto load = [&](uint32_t (&r)[32], uint32_t u) {
-        const uint32_t *src = in + (size_t)L.load_poly(u, npoly) * P::N + L.brl;
+        const uint32_t *src = in + LT::unit_base(u) + L.col_load(u, npoly);
         if constexpr (BR) src += LT::BIG ? 32 * L.h : 0u;   // brl + 32 h = l5 + 64 h (p1s_off)
         load32(r, src, [](int j) { return BR ? p1s_off<P>(j) : brv5(j) * LT::S; });
     };
@@ -587,7 +653,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_inv(const ui
     };
     auto back = [&](uint32_t (&r)[32], uint32_t u) {
         const uint32_t poly = L.poly(u);
-        uint32_t *dst = out + (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
+        uint32_t *dst = out + LT::unit_base(u) + L.col();   // pass-1 layout: natural lane index
         const bool valid = LT::BIG || poly < npoly;
         auto emit = [&](int j, uint32_t v) {
             if (valid) st_out(dst + LT::S * j, v);
@@ -616,14 +682,14 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_bitrev(const uin
     uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
     auto load = [&](uint32_t (&r)[32], uint32_t u) {
-        load32(r, in + (size_t)L.load_poly(u, npoly) * P::N + L.brl + (LT::BIG ? 32 * L.h : 0u),
+        load32(r, in + LT::unit_base(u) + L.col_load(u, npoly) + (LT::BIG ? 32 * L.h : 0u),
                [](int j) { return p1s_off<P>(j); });
     };
     auto process = [&](uint32_t (&r)[32], uint32_t u) {
         lds_p1_to_p2<P>(r, buf, L);
         const uint32_t poly = L.poly(u);
         if (LT::BIG || poly < npoly) {
-            uint32_t *dst = out + (size_t)poly * P::N + L.brl;
+            uint32_t *dst = out + LT::unit_base(u) + L.col();
 #pragma unroll
             for (int j = 0; j < 32; ++j) st_out(dst + brv5(j) * LT::S, r[j]);
         }
@@ -631,11 +697,14 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_bitrev(const uin
     chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
 }
 
-// fused c = a*b mod (x^n+1): FWD(a), FWD(b), Montgomery pointwise (the 2^-32
-// is folded into the inverse's final n^-1 scaling), INV -- one HBM read of a
-// and b, one write of c.  BHAT: b is given already transformed (natural-order
-// output of poly_ntt), so only a is transformed -- two transforms of work per
-// product instead of three (poly_mul_ntt).  a, b and c may alias (no
+// fused c = a*b mod (x^n+1): FWD(a), FWD(b) down to residues mod x^4 -+ zeta,
+// their products (basemul4; the 2^-32 of its REDC and the (n/4)^-1 are folded
+// into the inverse's final scaling), INV from those residues -- one HBM read
+// of a and b, one write of c.  The internal domain never leaves the kernel,
+// so it need not be poly_ntt's.  BHAT: b is given already transformed
+// (natural-order output of poly_ntt, the full domain), so a is transformed
+// completely and multiplied pointwise (Montgomery) -- two transforms of work
+// per product instead of three (poly_mul_ntt).  a, b and c may alias (no
 // __restrict__): every lane loads its words before it stores any.
 template <int PS, bool BHAT>
 __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
@@ -654,42 +723,49 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
     uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
 
     const uint32_t nunits = (npoly + LT::UPW - 1) / LT::UPW;
-    uint32_t u = blockIdx.x * (WAVES * ppw) + (threadIdx.x >> 6);
+    uint32_t u = blockIdx.x * (WAVES * ppw) + wave_id();
 #pragma unroll 1
     for (uint32_t it = 0; it < ppw; ++it, u += WAVES) {   // dispatch-ordered chunk (see chunk_loop)
         if (u >= nunits) break;
         const uint32_t poly = L.poly(u);
         const bool valid = poly < npoly;
-        const size_t off = (size_t)poly * P::N + L.brl;   // pass-1 layout: natural lane index
-        const size_t loff = (size_t)L.load_poly(u, npoly) * P::N + L.brl;
+        const size_t ubase = LT::unit_base(u);
+        // pass-1 layout: natural lane index.  Opaque per unit, so the lane
+        // offsets are not folded into loop-invariant 64-bit addresses (which
+        // pin VGPRs): the accesses keep the scalar base + 32-bit offset form
+        uint32_t off = L.col(), loff = L.col_load(u, npoly);
+        if constexpr (!BHAT) asm volatile("" : "+v"(off), "+v"(loff));
         // a first, then b: the transpose's memory fences keep b's loads below
         // a's transform, so only ~64 coefficients are live at the peak
         uint32_t ra[32], rb[32];
-        load32(ra, a + loff, [](int j) { return LT::S * j; });
+        load32(ra, a + ubase + loff, [](int j) { return LT::S * j; });
         fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
-        lds_p1_to_p2<P>(ra, buf, L);
-        fwd_pass2<P>(ra, ftw2 + opaque_zero(), L.lane);
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            ra[j] = csub<P::Q2>(ra[j]);
-            // b-hat is in natural order: register j of the pass-2 layout holds
-            // index brv5(j)*S + lane (the forward's store mapping)
-            rb[j] = ld_in(b + loff + LT::S * (BHAT ? brv5(j) : (uint32_t)j));
-        }
-        if constexpr (!BHAT) {
-            fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
-            lds_p1_to_p2<P>(rb, buf, L);
-            fwd_pass2<P>(rb, ftw2 + opaque_zero(), L.lane);
-        }
-#pragma unroll
-        for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(ra[j], csub<P::Q2>(rb[j]));   // b-hat < 2q
-        inv_pass2<P>(ra, itw2 + opaque_zero(), L.lane);
-        lds_p2_to_p1<P>(ra, buf, L);
-        uint32_t *pc = c + off;
+        lds_p1_to_p2<P>(ra, buf, BHAT ? L : LT(opaque_lane()));
+        fwd_pass2<P, BHAT ? 0 : 2>(ra, ftw2 + opaque_zero(), L.lane);
+        // b-hat is in natural order: register j of the pass-2 layout holds
+        // index brv5(j)*S + lane (the forward's store mapping)
+        load32(rb, b + ubase + loff, [](int j) { return LT::S * (BHAT ? brv5(j) : (uint32_t)j); });
+        uint32_t *pc = c + ubase + off;
         auto emit = [&](int j, uint32_t v) {   // stores interleaved with the last stage (see inv_pass1)
             if (valid) st_out(pc + LT::S * j, v);
         };
-        inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
+        if constexpr (!BHAT) {
+            // incomplete domain: both forwards stop above pos bit 1, products
+            // mod x^4 -+ zeta, the inverse starts at pos bit 2 (basemul4)
+            fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+            lds_p1_to_p2<P>(rb, buf, LT(opaque_lane()));
+            fwd_pass2<P, 2>(rb, ftw2 + opaque_zero(), L.lane);
+            basemul4<P>(ra, rb, ftw2 + opaque_zero(), L.lane);
+            inv_pass2<P, 2>(ra, itw2 + opaque_zero(), L.lane);
+            lds_p2_to_p1<P>(ra, buf, LT(opaque_lane()));
+            inv_pass1<PS, P, P::NINV4_R, P::C1_4R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(csub<P::Q2>(ra[j]), csub<P::Q2>(rb[j]));   // b-hat < 2q
+            inv_pass2<P>(ra, itw2 + opaque_zero(), L.lane);
+            lds_p2_to_p1<P>(ra, buf, L);
+            inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
+        }
     }
 }
 

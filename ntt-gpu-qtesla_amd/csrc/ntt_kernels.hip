@@ -98,7 +98,7 @@ Launch launch_for(Op op, int ps, size_t npoly, const DevInfo &d)
 {
     const size_t upw = param_set(ps)->logn == 11 ? 1 : 2;
     const size_t units = (npoly + upw - 1) / upw;
-    const size_t waves = (size_t)(op == OP_MUL ? (param_set(ps)->logn == 11 ? MUL_WG_BIG : MUL_WG) : NTT_WG) / 64;
+    const size_t waves = (size_t)(op == OP_MUL ? MUL_WG : NTT_WG) / 64;
     const size_t min_groups = (size_t)d.cus * NTT_MIN_WG_PER_CU;
     size_t ppw = units / (waves * min_groups);
     ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
@@ -373,7 +373,7 @@ int ntt_build_info(char *buf, size_t len)
         "qtesla_ntt gfx950: 1 launch/op, wave-per-poly (n=2048) / half-wave-per-poly (n=1024), 32 coeff/lane, "
         "LDS XOR-swizzled transpose, permlane32 bit-5 stage, Shoup/Harvey lazy CT + signed-Shoup GS butterflies, "
         "dispatch-ordered unit chunks; wg=" QNTT_STR(NTT_WG)
-        " mul_wg=" QNTT_STR(MUL_WG) "/" QNTT_STR(MUL_WG_BIG) " ppw<=" QNTT_STR(NTT_PPW_MAX)
+        " mul_wg=" QNTT_STR(MUL_WG) " ppw<=" QNTT_STR(NTT_PPW_MAX)
         " min_wg/cu=" QNTT_STR(NTT_MIN_WG_PER_CU) "; src=" QNTT_SRC_HASH;
     const int n = (int)strlen(s);
     if (!buf || !len) return n;
