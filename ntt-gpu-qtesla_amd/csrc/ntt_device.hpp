@@ -367,7 +367,7 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
 }
 
 // BMIN > 0 stops short: the stages on pos bits BMIN-1..0 are left out
-// (poly_mul's incomplete transform, basemul4)
+// (poly_mul's incomplete transform, BaseMul)
 template <class P, int BMIN = 0>
 __device__ __forceinline__ void fwd_pass2(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
 {
@@ -402,49 +402,58 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
     }
 }
 
-// Products in the incomplete NTT domain of poly_mul: after the forward's
-// stages down to pos bit 2, register group g = j>>2 of a lane holds the
-// residue of its polynomial mod x^4 - zeta (coefficient i in register 4g+i),
-// zeta = +w for g even and -w for g odd, w = psi^brv(k) the twiddle of the
-// stage on pos bit 2 (LDS entry 3 + (g>>1)).  Per residue: a, b canonical,
-// b~_i = zeta b_i (negated Shoup product, two-candidate min), the four sums
-// of four products in 64 bits (< 4q^2) and one Montgomery REDC each,
-// (c + m q) / 2^32 with m = -c q^-1 mod 2^32 (one v_mad_u64_u32): output in
-// [0, 2q), times 2^-32 (folded into the final scaling, NINV4_R).  Replaces
-// the forward's last two stages on both operands, the inverse's first two
-// and the pointwise product: ~430 fewer VALU per unit.
-template <class P>
-__device__ __forceinline__ void basemul4(uint32_t (&ra)[32], const uint32_t (&rb)[32], const uint2 *tab, uint32_t lane)
-{
-    static_assert(4.0 * P::Q * (double)P::Q + 4294967296.0 * P::Q < 18446744073709551616.0, "REDC input fits 64 bits");
-    static_assert(4.0 * P::Q * (double)P::Q / 4294967296.0 + P::Q < 2.0 * P::Q, "REDC output below 2q");
+// Products in the incomplete NTT domain of poly_mul.  After the forward's
+// stages down to pos bit LOGR, register group g = j >> LOGR of a lane holds
+// the residue of its polynomial mod x^D - zeta, D = 2^LOGR (coefficient i in
+// register D g + i), zeta = +w for g even and -w for g odd, w = psi^brv(k) the
+// twiddle of the stage on pos bit LOGR (LDS entry 2^(4-LOGR) - 1 + (g >> 1)).
+// Per residue: a, b canonical, b~_i = zeta b_i (negated Shoup product,
+// two-candidate min, in [0, q]), the D sums of D products in 64 bits
+// (< D q^2) and one Montgomery REDC each, (c + m q) / 2^32 with
+// m = -c q^-1 mod 2^32 (one v_mad_u64_u32), times 2^-32 (folded into the
+// final scaling with (n/D)^-1); outputs above 2q get one conditional
+// subtraction.  Replaces LOGR stages of each forward and of the inverse and
+// the pointwise product.
+template <class P, int LOGR>
+struct BaseMul {
+    static constexpr int D = 1 << LOGR;
+    static constexpr double QD = P::Q;
+    static_assert(D * QD * QD + 4294967296.0 * QD < 18446744073709551616.0, "REDC input fits 64 bits");
+    // REDC output bound D q^2 / 2^32 + q: below 2q, or below 4q with a csub
+    static constexpr bool OUT_CSUB = D * QD * QD / 4294967296.0 + QD >= 2.0 * QD;
+    static_assert(D * QD * QD / 4294967296.0 + QD < 4.0 * QD, "one conditional subtraction reaches [0, 2q)");
+    static constexpr int E0 = (1 << (4 - LOGR)) - 1;   // LDS entry of the stage on pos bit LOGR
+
+    static __device__ __forceinline__ void run(uint32_t (&ra)[32], const uint32_t (&rb)[32], const uint2 *tab, uint32_t lane)
+    {
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-        const uint2 w = tab[(3 + (g >> 1)) * 64 + lane];   // (-w mod 2^32, w')
-        uint32_t a[4], b[4], bt[4];
+        for (int g = 0; g < 32 / D; ++g) {
+            const uint2 w = tab[(E0 + (g >> 1)) * 64 + lane];   // (-w mod 2^32, w')
+            uint32_t a[D], b[D], bt[D];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            a[i] = canon4<P>(ra[4 * g + i]);
-            b[i] = canon4<P>(rb[4 * g + i]);
-        }
+            for (int i = 0; i < D; ++i) {
+                a[i] = canon4<P>(ra[D * g + i]);
+                b[i] = canon4<P>(rb[D * g + i]);
+            }
 #pragma unroll
-        for (int i = 1; i < 4; ++i) {
-            const uint32_t tn = madlo32(__umulhi(rb[4 * g + i], w.y), P::Q, rb[4 * g + i] * w.x);   // -(b w mod q), in (-2q, 0]
-            // zeta b_i as a value in [0, q]: +w -> min(-tn, -tn - q); -w -> min(tn + q, tn + 2q)
-            bt[i] = (g & 1) ? umin(tn + P::Q, tn + P::Q2) : umin(0u - tn, (0u - P::Q) - tn);
-        }
-        uint64_t c[4];
-        c[0] = (uint64_t)a[0] * b[0] + (uint64_t)a[1] * bt[3] + (uint64_t)a[2] * bt[2] + (uint64_t)a[3] * bt[1];
-        c[1] = (uint64_t)a[0] * b[1] + (uint64_t)a[1] * b[0] + (uint64_t)a[2] * bt[3] + (uint64_t)a[3] * bt[2];
-        c[2] = (uint64_t)a[0] * b[2] + (uint64_t)a[1] * b[1] + (uint64_t)a[2] * b[0] + (uint64_t)a[3] * bt[3];
-        c[3] = (uint64_t)a[0] * b[3] + (uint64_t)a[1] * b[2] + (uint64_t)a[2] * b[1] + (uint64_t)a[3] * b[0];
+            for (int i = 1; i < D; ++i) {
+                const uint32_t y = rb[D * g + i];
+                const uint32_t tn = madlo32(__umulhi(y, w.y), P::Q, y * w.x);   // -(b w mod q), in (-2q, 0]
+                // zeta b_i in [0, q]: +w -> min(-tn, -tn - q); -w -> min(tn + q, tn + 2q)
+                bt[i] = (g & 1) ? umin(tn + P::Q, tn + P::Q2) : umin(0u - tn, (0u - P::Q) - tn);
+            }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t m = (uint32_t)c[i] * P::QNEG;
-            ra[4 * g + i] = (uint32_t)(((uint64_t)m * P::Q + c[i]) >> 32);
+            for (int k = 0; k < D; ++k) {
+                uint64_t c = 0;
+#pragma unroll
+                for (int i = 0; i < D; ++i) c += (uint64_t)a[i] * (i <= k ? b[k - i] : bt[k + D - i]);
+                const uint32_t m = (uint32_t)c * P::QNEG;
+                const uint32_t r = (uint32_t)(((uint64_t)m * P::Q + c) >> 32);
+                ra[D * g + k] = OUT_CSUB ? csub<P::Q2>(r) : r;
+            }
         }
     }
-}
+};
 
 struct NoEmit {
     __device__ __forceinline__ void operator()(int, uint32_t) const {}
@@ -558,6 +567,15 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
 // incomplete-domain product and the per-transpose address recomputation
 // (fresh lanes) brought it under 128 VGPRs: 4 waves/SIMD is 4 % faster there
 // (poly_mul_ntt 8 %), profiles/r02/ab_polymul_incomplete.log
+// poly_mul's residue degree 2^LOGR: 8 (3 stages of each transform replaced
+// by 8x8 products) is 3 % faster than 4 on p-III and 6 % on p-I; 16 spills
+// (profiles/r02/ab_polymul_incomplete.log)
+#ifndef MUL_LOGR
+#define MUL_LOGR 3
+#endif
+#ifndef MUL_LOGR_SMALL
+#define MUL_LOGR_SMALL MUL_LOGR
+#endif
 #ifndef MUL_WG
 #define MUL_WG 1024
 #endif
@@ -569,6 +587,7 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
 #endif
 template <int PS> constexpr int mul_wg() { return MUL_WG; }
 template <int PS> constexpr int mul_occ() { return MUL_WAVES_PER_SIMD; }
+template <int PS> constexpr int mul_logr() { return PSel<PS>::T::LOGN == 11 ? MUL_LOGR : MUL_LOGR_SMALL; }
 constexpr int WG = 256;   // elementwise kernels
 constexpr int NTT_WAVES = NTT_WG / 64;
 constexpr int NTT_LDS_WORDS = NTT_WAVES * XPOSE_WORDS + TW2_WORDS;
@@ -697,8 +716,8 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_bitrev(const uin
     chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
 }
 
-// fused c = a*b mod (x^n+1): FWD(a), FWD(b) down to residues mod x^4 -+ zeta,
-// their products (basemul4; the 2^-32 of its REDC and the (n/4)^-1 are folded
+// fused c = a*b mod (x^n+1): FWD(a), FWD(b) down to residues mod x^8 -+ zeta,
+// their products (BaseMul; the 2^-32 of its REDC and the (n/8)^-1 are folded
 // into the inverse's final scaling), INV from those residues -- one HBM read
 // of a and b, one write of c.  The internal domain never leaves the kernel,
 // so it need not be poly_ntt's.  BHAT: b is given already transformed
@@ -741,7 +760,7 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
         load32(ra, a + ubase + loff, [](int j) { return LT::S * j; });
         fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
         lds_p1_to_p2<P>(ra, buf, BHAT ? L : LT(opaque_lane()));
-        fwd_pass2<P, BHAT ? 0 : 2>(ra, ftw2 + opaque_zero(), L.lane);
+        fwd_pass2<P, BHAT ? 0 : mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
         // b-hat is in natural order: register j of the pass-2 layout holds
         // index brv5(j)*S + lane (the forward's store mapping)
         load32(rb, b + ubase + loff, [](int j) { return LT::S * (BHAT ? brv5(j) : (uint32_t)j); });
@@ -750,15 +769,16 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
             if (valid) st_out(pc + LT::S * j, v);
         };
         if constexpr (!BHAT) {
-            // incomplete domain: both forwards stop above pos bit 1, products
-            // mod x^4 -+ zeta, the inverse starts at pos bit 2 (basemul4)
+            // incomplete domain: both forwards stop above pos bit LOGR-1,
+            // products mod x^(2^LOGR) -+ zeta, the inverse starts at pos bit
+            // LOGR (BaseMul)
             fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
             lds_p1_to_p2<P>(rb, buf, LT(opaque_lane()));
-            fwd_pass2<P, 2>(rb, ftw2 + opaque_zero(), L.lane);
-            basemul4<P>(ra, rb, ftw2 + opaque_zero(), L.lane);
-            inv_pass2<P, 2>(ra, itw2 + opaque_zero(), L.lane);
+            fwd_pass2<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
+            BaseMul<P, mul_logr<PS>()>::run(ra, rb, ftw2 + opaque_zero(), L.lane);
+            inv_pass2<P, mul_logr<PS>()>(ra, itw2 + opaque_zero(), L.lane);
             lds_p2_to_p1<P>(ra, buf, LT(opaque_lane()));
-            inv_pass1<PS, P, P::NINV4_R, P::C1_4R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
+            inv_pass1<PS, P, P::template ninv_r<mul_logr<PS>()>(), P::template c1_r<mul_logr<PS>()>()>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
         } else {
 #pragma unroll
             for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(csub<P::Q2>(ra[j]), csub<P::Q2>(rb[j]));   // b-hat < 2q

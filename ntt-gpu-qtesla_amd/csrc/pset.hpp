@@ -51,10 +51,10 @@ struct PSet {
     static constexpr uint32_t R = (uint32_t)((1ull << 32) % Q_);
     static constexpr uint32_t NINV_R = (uint32_t)((uint64_t)NINV * R % Q_);
     static constexpr uint32_t C1_R = (uint32_t)((uint64_t)C1 * R % Q_);
-    // poly_mul's inverse runs 2 stages short (residues mod x^4 - zeta, see
-    // basemul4): its final scaling is (n/4)^-1 = 4 n^-1
-    static constexpr uint32_t NINV4_R = (uint32_t)(4ull * NINV_R % Q_);
-    static constexpr uint32_t C1_4R = (uint32_t)(4ull * C1_R % Q_);
+    // poly_mul's inverse runs LOGR stages short (residues mod x^(2^LOGR) -
+    // zeta, see BaseMul): its final scaling is (n / 2^LOGR)^-1
+    template <int LOGR> static constexpr uint32_t ninv_r() { return (uint32_t)((1ull << LOGR) * NINV_R % Q_); }
+    template <int LOGR> static constexpr uint32_t c1_r() { return (uint32_t)((1ull << LOGR) * C1_R % Q_); }
 };
 using PS0 = PSet<8404993u, 10, 2083362u>;
 using PS1 = PSet<343576577u, 10, cpow(3, (343576577u - 1) / 2048, 343576577u)>;
