@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "ntt_device.hpp"
+#include "ntt_large.hpp"
 #include "params.hpp"
 
 namespace qntt {
@@ -40,25 +41,78 @@ inline std::vector<uint32_t> dev_const_table(const ParamSet &p, const Tables &t,
 
 // LDS image (fill_tw2): entry e of stage bit b = tw2_b(e), lane t holds twiddle
 // k = 2^(logn-1-b) + (Lp << (4-b)) + m with Lp = bitrev(lane) (see Lane);
-// then the 32 bit-5 twiddles k = 32 + i.
-inline std::vector<uint32_t> dev_tw2_image(const ParamSet &p, const Tables &t, bool inv)
+// then the 32 bit-5 twiddles k = 32 + i.  `logn` is the geometry's (the
+// 2048-point one for the large-n sub-trees) and kmap(k) the index in the
+// direction's table (identity for n <= 2048).
+template <class KMap>
+inline std::vector<uint32_t> dev_tw2_image(const ParamSet &p, const Tables &t, bool inv, uint32_t logn, KMap kmap)
 {
     std::vector<uint32_t> o(TW2_WORDS, 0);
-    auto put = [&](int slot, uint32_t k) { dev_pair(p, t, inv, k, o[2 * slot], o[2 * slot + 1]); };
+    auto put = [&](int slot, uint32_t k) { dev_pair(p, t, inv, kmap(k), o[2 * slot], o[2 * slot + 1]); };
     for (int e = 0; e < TW2_ENTRIES; e++) {
         const int b = e < 1 ? 4 : e < 3 ? 3 : e < 7 ? 2 : e < 15 ? 1 : 0;
         const uint32_t m = e - ((1u << (4 - b)) - 1);
         for (uint32_t lane = 0; lane < 64; lane++) {
-            const uint32_t Lp = p.logn == 11 ? bitrev(lane, 6) : bitrev(lane & 31, 5);
-            put(e * 64 + lane, (1u << (p.logn - 1 - b)) + (Lp << (4 - b)) + m);
+            const uint32_t Lp = logn == 11 ? bitrev(lane, 6) : bitrev(lane & 31, 5);
+            put(e * 64 + lane, (1u << (logn - 1 - b)) + (Lp << (4 - b)) + m);
         }
     }
     for (int i = 0; i < 32; i++) put(TW2_ENTRIES * 64 + i, 32u + i);
     return o;
 }
+inline std::vector<uint32_t> dev_tw2_image(const ParamSet &p, const Tables &t, bool inv)
+{
+    return dev_tw2_image(p, t, inv, p.logn, [](uint32_t k) { return k; });
+}
 
-// Upload every table of the three parameter sets to the current device.
-inline hipError_t upload_device_tables(const Tables *tabs /* [3] */)
+// Large n = G * 2048: twiddle index k' of sub-tree B's 2048-point transform
+// in the n-point table, k' = 2^s + m -> 2^s (G + B) + m (ntt_large.hpp)
+inline uint32_t sub_tree_k(uint32_t kp, uint32_t G, uint32_t B)
+{
+    if (kp == 0) return 0;
+    const uint32_t s = 31 - __builtin_clz(kp);
+    return (kp - (1u << s)) + (1u << s) * (G + B);
+}
+
+// Tables of the large-n kernels of param set ps (3 or 4) to the current device
+inline hipError_t upload_large_tables(int ps, const Tables &t)
+{
+    const ParamSet &p = *param_set(ps);
+    const int idx = ps - LARGE_PS0;
+    const uint32_t G = p.n / 2048;
+    hipError_t e;
+    for (int inv = 0; inv < 2; inv++) {
+        uint2 sub[LARGE_GMAX][32] = {}, cross[4] = {};
+        for (uint32_t B = 0; B < G; B++) {
+            for (uint32_t kp = 0; kp < 32; kp++)
+                dev_pair(p, t, inv != 0, sub_tree_k(kp, G, B), sub[B][kp].x, sub[B][kp].y);
+            const std::vector<uint32_t> img =
+                dev_tw2_image(p, t, inv != 0, 11, [&](uint32_t kp) { return sub_tree_k(kp, G, B); });
+            const size_t off = ((size_t)(idx * 2 + inv) * LARGE_GMAX + B) * TW2_VEC4 * 16;
+            if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_tw2imgL), img.data(), TW2_WORDS * 4, off, hipMemcpyHostToDevice)) !=
+                hipSuccess)
+                return e;
+        }
+        for (uint32_t k = 1; k < G; k++) dev_pair(p, t, inv != 0, k, cross[k].x, cross[k].y);
+        if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_subtw), sub, sizeof sub, (size_t)(idx * 2 + inv) * sizeof sub,
+                                   hipMemcpyHostToDevice)) != hipSuccess)
+            return e;
+        if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_cross), cross, sizeof cross, (size_t)(idx * 2 + inv) * sizeof cross,
+                                   hipMemcpyHostToDevice)) != hipSuccess)
+            return e;
+    }
+    uint2 last[LARGE_GMAX] = {};
+    for (uint32_t B = 0; B < G; B++) {   // n^-1 psi^-brv(G + B), centred signed
+        const uint32_t w = (uint32_t)((uint64_t)t.n_inv * t.inv[2 * (G + B)] % p.q);
+        const TwPair c = csigned_tw(w, p.q);
+        last[B].x = c.x;
+        last[B].y = c.y;
+    }
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_lastinv), last, sizeof last, (size_t)idx * sizeof last, hipMemcpyHostToDevice);
+}
+
+// Upload every table of the parameter sets to the current device.
+inline hipError_t upload_device_tables(const Tables *tabs /* [NPARAM_SETS] */)
 {
     const void *syms[3][2] = {{HIP_SYMBOL(c_fwd0), HIP_SYMBOL(c_inv0)},
                               {HIP_SYMBOL(c_fwd1), HIP_SYMBOL(c_inv1)},
@@ -74,6 +128,10 @@ inline hipError_t upload_device_tables(const Tables *tabs /* [3] */)
                                   (size_t)(ps * 2 + inv) * TW2_WORDS * 4, hipMemcpyHostToDevice);
             if (e != hipSuccess) return e;
         }
+    for (int ps = LARGE_PS0; ps < LARGE_PS0 + LARGE_NPS; ps++) {
+        const hipError_t e = upload_large_tables(ps, tabs[ps]);
+        if (e != hipSuccess) return e;
+    }
     return hipSuccess;
 }
 

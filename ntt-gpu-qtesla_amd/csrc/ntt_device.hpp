@@ -336,10 +336,12 @@ __device__ __forceinline__ void fill_tw2(uint2 *tab)
 // ------------------------------------------------------------------------
 // forward pass 1: CT stages on pos bits LOGN-1 .. LOGN-5 (j bits 4..0),
 // twiddle index k = 2^s + (j >> (5-s)) -- wave-uniform.
-template <int PS, class P>
-__device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw)
+// `tw` = the uniform twiddles k < 32 (wave-uniform pointer), `sw` = the
+// 32-entry bit-5 table in LDS.  RED0: inputs in [0,4q) (stage 0 reduces too);
+// otherwise inputs < 2q.
+template <class P, bool RED0 = false>
+__device__ __forceinline__ void fwd_pass1_tw(uint32_t (&r)[32], uint32_t h, const uint2 *tw, const uint2 *sw)
 {
-    const uint2 *tw = tw_base<PS, false>();
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
         const int hh = 16 >> s;
@@ -347,7 +349,7 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
         for (int j = 0; j < 32; ++j) {
             if ((j & hh) == 0) {
                 const uint2 w = tw[(1u << s) + (uint32_t)(j >> (5 - s))];
-                if (s == 0) ct_bfly<P::Q, false>(r[j], r[j + hh], w.x, w.y);   // inputs < 2q
+                if (s == 0 && !RED0) ct_bfly<P::Q, false>(r[j], r[j + hh], w.x, w.y);   // inputs < 2q
                 else ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
             }
         }
@@ -364,6 +366,12 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
             ct_bfly<P::Q>(r[2 * m], r[2 * m + 1], w.x, w.y);
         }
     }
+}
+
+template <int PS, class P>
+__device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw)
+{
+    fwd_pass1_tw<P>(r, h, tw_base<PS, false>(), sw);
 }
 
 // BMIN > 0 stops short: the stages on pos bits BMIN-1..0 are left out
@@ -459,16 +467,12 @@ struct NoEmit {
     __device__ __forceinline__ void operator()(int, uint32_t) const {}
 };
 
-// inverse pass 1: (n=2048) GS on pos bit 5 + swap back, then GS stages on pos
-// bits LOGN-5 .. LOGN-1 (j bits 0..4); the last one carries the n^-1 scaling
-// (times the S0 / S1 constants), output canonical.  `emit(j, v)` is called
-// with each final output as soon as it is computed (the kernels store from
-// there, so the 32 stores interleave with the last stage instead of queueing
-// behind it as one tail).
-template <int PS, class P, uint32_t S0, uint32_t S1, class Emit = NoEmit>
-__device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw, const Emit &emit = Emit())
+// inverse pass 1 without its last stage: (n=2048) GS on pos bit 5 + swap
+// back, then the GS stages on pos bits LOGN-5 .. LOGN-2 (j bits 0..3); `tw` =
+// the uniform twiddles k < 32.
+template <class P>
+__device__ __forceinline__ void inv_pass1_head(uint32_t (&r)[32], uint32_t h, const uint2 *tw, const uint2 *sw)
 {
-    const uint2 *tw = tw_base<PS, true>();
     if constexpr (P::LOGN == 11) {
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
@@ -490,20 +494,41 @@ __device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const u
             }
         }
     }
-    constexpr uint32_t S0P = cshoup(S0, P::Q);
-    constexpr TwPair S1S = csigned_tw(S1, P::Q);
+}
+
+// The last GS stage (pos bit LOGN-1, j bits 4): x' = (x+y) s0, y' = (x-y) s1
+// with s0 = (s0w, s0p) a Shoup pair and s1 = (s1w, s1p) a centred signed
+// pair (the stage's twiddle times the scaling), outputs in [0,2q), canonical
+// when CANON.  `emit(j, v)` is called with each final output as soon as it is
+// computed (the kernels store from there, so the 32 stores interleave with
+// the last stage instead of queueing behind it as one tail).
+template <class P, bool CANON, class Emit = NoEmit>
+__device__ __forceinline__ void inv_last_stage(uint32_t (&r)[32], uint32_t s0w, uint32_t s0p, uint32_t s1w, uint32_t s1p,
+                                               const Emit &emit = Emit())
+{
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint32_t x = r[j], y = r[j + 16];
         const uint32_t s = x + y;   // [0,4q)
         const uint32_t d = x - y;   // (-2q, 2q), signed
-        const uint32_t a = shoup_mul<P::Q>(s, S0, S0P);
-        const uint32_t b = sshoup_mul<P::Q>(d, S1S.x, S1S.y);
-        r[j] = csub<P::Q>(a);
-        r[j + 16] = csub<P::Q>(b);
+        const uint32_t a = shoup_mul<P::Q>(s, s0w, s0p);
+        const uint32_t b = sshoup_mul<P::Q>(d, s1w, s1p);
+        r[j] = CANON ? csub<P::Q>(a) : a;
+        r[j + 16] = CANON ? csub<P::Q>(b) : b;
         emit(j, r[j]);
         emit(j + 16, r[j + 16]);
     }
+}
+
+// inverse pass 1: the head, then the last stage with the n^-1 scaling (times
+// the S0 / S1 constants), output canonical.
+template <int PS, class P, uint32_t S0, uint32_t S1, class Emit = NoEmit>
+__device__ __forceinline__ void inv_pass1(uint32_t (&r)[32], uint32_t h, const uint2 *sw, const Emit &emit = Emit())
+{
+    inv_pass1_head<P>(r, h, tw_base<PS, true>(), sw);
+    constexpr uint32_t S0P = cshoup(S0, P::Q);
+    constexpr TwPair S1S = csigned_tw(S1, P::Q);
+    inv_last_stage<P, true>(r, S0, S0P, S1S.x, S1S.y, emit);
 }
 
 // ------------------------------------------------------------------------

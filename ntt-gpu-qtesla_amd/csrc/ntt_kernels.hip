@@ -12,6 +12,7 @@
 #include "../../include/qtesla_ntt.h"
 #include "dev_tables.hpp"
 #include "ntt_device.hpp"
+#include "ntt_large.hpp"
 #include "ntt_internal.h"
 #include "params.hpp"
 #include "pset.hpp"
@@ -36,12 +37,12 @@ int hip_err(hipError_t e)
 constexpr int kMaxDev = 64;
 
 std::once_flag g_cpu_tables_once;
-Tables g_cpu_tables[3];
+Tables g_cpu_tables[NPARAM_SETS];
 
 const Tables &cpu_tables(int ps)
 {
     std::call_once(g_cpu_tables_once, [] {
-        for (int i = 0; i < 3; i++) make_tables(*param_set(i), g_cpu_tables[i]);
+        for (int i = 0; i < NPARAM_SETS; i++) make_tables(*param_set(i), g_cpu_tables[i]);
     });
     return g_cpu_tables[ps];
 }
@@ -73,8 +74,7 @@ int device_ready(DevInfo **out)
         d.geo = true;
     }
     if (!d.tables) {
-        const Tables tabs[3] = {cpu_tables(0), cpu_tables(1), cpu_tables(2)};
-        if ((e = upload_device_tables(tabs)) != hipSuccess) return hip_err(e);
+        if ((e = upload_device_tables(&cpu_tables(0))) != hipSuccess) return hip_err(e);
         d.tables = true;
     }
     *out = &d;
@@ -139,6 +139,8 @@ int dispatch(int ps, Args... args)
     case 0: return Launcher<0>::run(args...);
     case 1: return Launcher<1>::run(args...);
     case 2: return Launcher<2>::run(args...);
+    case 3: return Launcher<3>::run(args...);
+    case 4: return Launcher<4>::run(args...);
     default: return NTT_ERR_PARAM;
     }
 }
@@ -150,15 +152,25 @@ enum Xform { FWD, INV, FWD_BR, INV_BR, BITREV };
 template <int PS> struct LXform {
     static int run(Xform k, const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s, const DevInfo &d)
     {
-        const Launch l = launch_for(OP_XFORM, PS, batch, d);
-        const dim3 g(l.grid), b(NTT_WG);
-        const uint32_t nb = (uint32_t)batch;
-        switch (k) {
-        case FWD: hipLaunchKernelGGL((k_ntt_fwd<PS, false>), g, b, 0, s, in, out, nb, l.ppw); break;
-        case INV: hipLaunchKernelGGL((k_ntt_inv<PS, false>), g, b, 0, s, in, out, nb, l.ppw); break;
-        case FWD_BR: hipLaunchKernelGGL((k_ntt_fwd<PS, true>), g, b, 0, s, in, out, nb, l.ppw); break;
-        case INV_BR: hipLaunchKernelGGL((k_ntt_inv<PS, true>), g, b, 0, s, in, out, nb, l.ppw); break;
-        case BITREV: hipLaunchKernelGGL(k_bitrev<PS>, g, b, 0, s, in, out, nb, l.ppw); break;
+        if constexpr (PS >= LARGE_PS0) {   // n = 4096 / 8192: natural-order transforms only
+            using LG = Large<PS>;
+            if (k != FWD && k != INV) return NTT_ERR_PARAM;
+            size_t ppw = batch / ((size_t)LG::SLOTS * d.cus * 2);
+            ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
+            const dim3 g((uint32_t)((batch + LG::SLOTS * ppw - 1) / (LG::SLOTS * ppw))), b(LG::NT);
+            if (k == FWD) hipLaunchKernelGGL(k_ntt_fwd_large<PS>, g, b, 0, s, in, out, (uint32_t)batch, (uint32_t)ppw);
+            else hipLaunchKernelGGL(k_ntt_inv_large<PS>, g, b, 0, s, in, out, (uint32_t)batch, (uint32_t)ppw);
+        } else {
+            const Launch l = launch_for(OP_XFORM, PS, batch, d);
+            const dim3 g(l.grid), b(NTT_WG);
+            const uint32_t nb = (uint32_t)batch;
+            switch (k) {
+            case FWD: hipLaunchKernelGGL((k_ntt_fwd<PS, false>), g, b, 0, s, in, out, nb, l.ppw); break;
+            case INV: hipLaunchKernelGGL((k_ntt_inv<PS, false>), g, b, 0, s, in, out, nb, l.ppw); break;
+            case FWD_BR: hipLaunchKernelGGL((k_ntt_fwd<PS, true>), g, b, 0, s, in, out, nb, l.ppw); break;
+            case INV_BR: hipLaunchKernelGGL((k_ntt_inv<PS, true>), g, b, 0, s, in, out, nb, l.ppw); break;
+            case BITREV: hipLaunchKernelGGL(k_bitrev<PS>, g, b, 0, s, in, out, nb, l.ppw); break;
+            }
         }
         return finish_launch();
     }
@@ -167,11 +179,15 @@ template <int PS> struct LMul {
     static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s, bool bhat,
                    const DevInfo &d)
     {
-        const Launch l = launch_for(OP_MUL, PS, batch, d);
-        const dim3 g(l.grid), blk(mul_wg<PS>());
-        if (bhat) hipLaunchKernelGGL((k_poly_mul<PS, true>), g, blk, 0, s, a, b, c, (uint32_t)batch, l.ppw);
-        else hipLaunchKernelGGL((k_poly_mul<PS, false>), g, blk, 0, s, a, b, c, (uint32_t)batch, l.ppw);
-        return finish_launch();
+        if constexpr (PS >= LARGE_PS0) {
+            return NTT_ERR_PARAM;   // no fused product for n > 2048
+        } else {
+            const Launch l = launch_for(OP_MUL, PS, batch, d);
+            const dim3 g(l.grid), blk(mul_wg<PS>());
+            if (bhat) hipLaunchKernelGGL((k_poly_mul<PS, true>), g, blk, 0, s, a, b, c, (uint32_t)batch, l.ppw);
+            else hipLaunchKernelGGL((k_poly_mul<PS, false>), g, blk, 0, s, a, b, c, (uint32_t)batch, l.ppw);
+            return finish_launch();
+        }
     }
 };
 template <int PS> struct LPw {
@@ -190,6 +206,7 @@ int transform(Xform k, uint32_t *out, const uint32_t *in, size_t batch, int ps, 
     if (rc == NTT_OK && batch) rc = check_common(ps, out, batch);
     if (rc != NTT_OK || batch == 0) return rc;
     if (partial_overlap(in, out, batch * param_set(ps)->n * 4)) return NTT_ERR_ALIAS;
+    if (param_set(ps)->n > 2048 && k != FWD && k != INV) return NTT_ERR_PARAM;   // natural order only
     DevInfo *d = nullptr;
     if ((rc = device_ready(&d)) != NTT_OK) return rc;
     return dispatch<LXform>(ps, k, in, out, batch, (hipStream_t)stream, *d);
@@ -204,6 +221,7 @@ int mul_common(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t b
     if ((rc = check_common(ps, d_c, batch)) != NTT_OK) return rc;
     const size_t bytes = batch * param_set(ps)->n * 4;
     if (partial_overlap(d_a, d_c, bytes) || partial_overlap(d_b, d_c, bytes)) return NTT_ERR_ALIAS;
+    if (param_set(ps)->n > 2048) return NTT_ERR_PARAM;   // no fused product at n > 2048
     DevInfo *d = nullptr;
     if ((rc = device_ready(&d)) != NTT_OK) return rc;
     return dispatch<LMul>(ps, d_a, d_b, d_c, batch, (hipStream_t)stream, bhat, *d);
@@ -304,6 +322,7 @@ int poly_mul_nussbaumer(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b,
     int rc;
     if ((rc = check_common(ps, d_a, batch)) != NTT_OK) return rc;
     if (ring != NTT_RING_Q && ring != NTT_RING_M32) return NTT_ERR_PARAM;
+    if (param_set(ps)->n > 2048) return NTT_ERR_PARAM;   // Nussbaumer splits for n = 1024 / 2048
     if (batch == 0) return NTT_OK;
     if ((rc = check_common(ps, d_b, batch)) != NTT_OK) return rc;
     if ((rc = check_common(ps, d_c, batch)) != NTT_OK) return rc;

@@ -1,0 +1,221 @@
+// ntt_large.hpp -- gfx950 transforms for n = 4096 and n = 8192 (param sets 3
+// and 4, p-III's prime): the multi-wave four-step dataflow of SURVEY.md 8f
+// row 3 (the reference's alternatives for other sizes are its Stockham
+// kernels, NTT.cu:1085-1153 / 1268-1337, and CT2, :667-951).  Included by
+// ntt_kernels.hip after ntt_device.hpp (it owns the __constant__ symbols).
+//
+// One polynomial is split over G = n/2048 waves of a workgroup; wave B owns
+// sub-block B (pos = 2048 B + p').  CT DIT with merged twist, stages on pos
+// bits L-1 .. 0 (L = log2 n):
+//   * the first g = log2 G stages (pos bits L-1 .. 11) pair sub-block B with
+//     sub-block B ^ 2^(g-1-s): radix-2 stages ACROSS waves, one LDS exchange
+//     round each.  The wave holding the upper half sends t = w y (negated
+//     Shoup product), the lower one x mod 2q; each keeps one output, so no
+//     multiply is done twice;
+//   * sub-block B is then a 2048-point transform whose twiddles are its own
+//     sub-tree of the n-point table, T_B[2^s + m] = psi^brv(2^s (2^g + B) + m):
+//     the n = 2048 kernel's passes (register pass, permlane32 stage, LDS
+//     transpose, register pass) with per-wave twiddle tables;
+//   * natural-order output k' of sub-block B is global index G k' + brv_g(B):
+//     the G waves' stores interleave at a stride of G words.  They run
+//     together on one CU, so the partial lines merge in the L2.
+// The inverse runs in reverse: strided loads, the 2048-point GS passes with
+// T_B^-1 (n^-1 folded into their last stage), the g GS stages across waves
+// (LDS exchanges), contiguous stores.
+#pragma once
+#include "ntt_device.hpp"
+
+namespace qntt {
+
+constexpr int LARGE_PS0 = 3;    // first large-n param set
+constexpr int LARGE_NPS = 2;    // n = 4096, 8192
+constexpr int LARGE_GMAX = 4;   // waves per polynomial at n = 8192
+
+// uniform pass-1 twiddles (k' < 32) of sub-tree B, [set][fwd/inv][B][k']
+__constant__ uint2 c_subtw[LARGE_NPS][2][LARGE_GMAX][32];
+// twiddles k = 1 .. G-1 of the cross-wave stages, [set][fwd/inv][k]
+__constant__ uint2 c_cross[LARGE_NPS][2][4];
+// last sub-tree inverse stage: n^-1 psi^-brv(2^g + B), centred signed pair
+__constant__ uint2 c_lastinv[LARGE_NPS][LARGE_GMAX];
+// LDS images (lane twiddles + bit-5 table) of T_B, [set][fwd/inv][B]
+__device__ uint4 g_tw2imgL[LARGE_NPS][2][LARGE_GMAX][TW2_VEC4];
+
+template <int PS>
+struct Large {
+    using PL = typename PSel<PS>::T;   // the n-point set
+    using P = PS2;                     // 2048-point sub-transforms over the same prime
+    static_assert(PL::Q == P::Q, "large-n sets use p-III's prime");
+    static constexpr int G = (int)(PL::N / 2048);
+    static constexpr int LOGG = G == 2 ? 1 : 2;
+    // 16 waves x 8 KiB + 2 x 15.75 KiB tables / 12 waves x 8 KiB + 4 x 15.75
+    // KiB: one workgroup per CU, 4 / 3 waves per SIMD
+    static constexpr int WAVES = G == 2 ? 16 : 12;
+    static constexpr int OCC = WAVES / 4;
+    static constexpr int SLOTS = WAVES / G;   // polynomials per workgroup step
+    static constexpr int NT = WAVES * 64;
+    static constexpr int IDX = PS - LARGE_PS0;
+    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + G * TW2_WORDS;
+};
+
+// global-order offset of sub-block B's outputs: brv_g(B)
+__host__ __device__ constexpr uint32_t brv_g(uint32_t b, int logg) { return logg == 1 ? b : (((b & 1u) << 1) | (b >> 1)); }
+
+// One radix-2 CT stage across waves: this wave and its partner hold the two
+// halves at the same register/lane slots; `hi` = this wave holds the upper
+// (y) half.  lo sends a = x mod 2q (x itself when !RED: inputs < 2q), hi
+// sends tn = -(w y mod q); lo keeps a + t, hi keeps a - t + 2q, in [0,4q).
+// Exchange through the waves' own transpose buffers, layout [j][lane]
+// (conflict-free b32 accesses); the second barrier frees the buffers.
+template <class P, bool RED>
+__device__ __forceinline__ void cross_ct(uint32_t (&r)[32], uint32_t *mine, const uint32_t *theirs, uint32_t lane, bool hi,
+                                         uint2 w)
+{
+    if (hi) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) r[j] = madlo32(__umulhi(r[j], w.y), P::Q, r[j] * w.x);
+    } else if (RED) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) r[j] = csub<P::Q2>(r[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 32; ++j) mine[j * 64 + lane] = r[j];
+    __syncthreads();
+    if (hi) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) r[j] = theirs[j * 64 + lane] + r[j] + 2 * P::Q;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) r[j] = r[j] - theirs[j * 64 + lane];
+    }
+    __syncthreads();
+}
+
+// One GS stage across waves, inputs and outputs in [0,2q): lo keeps
+// (x + y) mod 2q, hi keeps (x - y) w by the signed Shoup product.
+template <class P>
+__device__ __forceinline__ void cross_gs(uint32_t (&r)[32], uint32_t *mine, const uint32_t *theirs, uint32_t lane, bool hi,
+                                         uint2 w)
+{
+#pragma unroll
+    for (int j = 0; j < 32; ++j) mine[j * 64 + lane] = r[j];
+    __syncthreads();
+    if (hi) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) r[j] = sshoup_mul<P::Q>(theirs[j * 64 + lane] - r[j], w.x, w.y);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) r[j] = csub<P::Q2>(r[j] + theirs[j * 64 + lane]);
+    }
+    __syncthreads();
+}
+
+// The workgroup's G lane-twiddle images of one direction (contiguous in
+// g_tw2imgL) into LDS after the transpose buffers.
+template <class LG, bool INV>
+__device__ __forceinline__ void fill_large_tw(uint32_t *lds)
+{
+    const uint4 *src = g_tw2imgL[LG::IDX][INV ? 1 : 0][0];
+    uint4 *dst = reinterpret_cast<uint4 *>(lds + LG::WAVES * XPOSE_WORDS);
+    for (int i = threadIdx.x; i < LG::G * TW2_VEC4; i += LG::NT) dst[i] = src[i];
+}
+
+// Workgroup b owns polynomials [b SLOTS ppw, (b+1) SLOTS ppw); slot s of a
+// step takes waves s G .. s G + G-1.  Every wave runs the workgroup's step
+// count (the exchanges hold barriers): slots past the batch recompute the
+// workgroup's first polynomial and store nothing.
+template <int PS>
+__global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large(const uint32_t *in, uint32_t *out,
+                                                                                uint32_t npoly, uint32_t ppw)
+{
+    using LG = Large<PS>;
+    using P = typename LG::P;
+    using LT = Lane<P>;
+    constexpr int G = LG::G;
+    constexpr uint32_t N = LG::PL::N;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
+    const uint32_t first = blockIdx.x * (LG::SLOTS * ppw);
+    if (first >= npoly) return;   // whole workgroup
+    const uint32_t wave = wave_id(), B = wave % G, slot = wave / G;
+    uint32_t *const buf = lds + wave * XPOSE_WORDS;
+    const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + B * TW2_WORDS);
+    fill_large_tw<LG, false>(lds);
+    __syncthreads();
+    const LT L;
+    const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
+    const uint32_t kout = brv_g(B, LG::LOGG);   // global index = G k' + kout
+#pragma unroll 1
+    for (uint32_t it = 0; it < steps; ++it) {
+        const uint32_t poly = first + it * LG::SLOTS + slot;
+        const bool valid = poly < npoly;
+        // lane offsets opaque per step: the accesses keep the scalar base +
+        // 32-bit offset form instead of loop-invariant 64-bit VGPR addresses
+        uint32_t lo = L.brl, so = G * L.brl;
+        asm volatile("" : "+v"(lo), "+v"(so));
+        uint32_t r[32];
+        load32(r, in + (size_t)(valid ? poly : first) * N + B * 2048u + lo, [](int j) { return 64 * j; });
+        // pos bit L-1 (k = 1), then for n = 8192 pos bit 11 (k = 2 + B/2)
+        constexpr uint32_t D0 = G / 2;
+        cross_ct<P, false>(r, buf, lds + (wave ^ D0) * XPOSE_WORDS, L.lane, (B & D0) != 0, c_cross[LG::IDX][0][1]);
+        if constexpr (G == 4)
+            cross_ct<P, true>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0,
+                              c_cross[LG::IDX][0][2 + (B >> 1)]);
+        fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        lds_p1_to_p2<P>(r, buf, L);
+        fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        if (valid) {
+            uint32_t *dst = out + (size_t)poly * N + kout + so;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) st_out(dst + G * 64 * brv5(j), canon4<P>(r[j]));
+        }
+    }
+}
+
+template <int PS>
+__global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large(const uint32_t *in, uint32_t *out,
+                                                                                uint32_t npoly, uint32_t ppw)
+{
+    using LG = Large<PS>;
+    using P = typename LG::P;
+    using LT = Lane<P>;
+    constexpr int G = LG::G;
+    constexpr uint32_t N = LG::PL::N;
+    constexpr uint32_t NINVP = cshoup(LG::PL::NINV, P::Q);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
+    const uint32_t first = blockIdx.x * (LG::SLOTS * ppw);
+    if (first >= npoly) return;
+    const uint32_t wave = wave_id(), B = wave % G, slot = wave / G;
+    uint32_t *const buf = lds + wave * XPOSE_WORDS;
+    const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + B * TW2_WORDS);
+    fill_large_tw<LG, true>(lds);
+    __syncthreads();
+    const LT L;
+    const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
+    const uint32_t kin = brv_g(B, LG::LOGG);
+#pragma unroll 1
+    for (uint32_t it = 0; it < steps; ++it) {
+        const uint32_t poly = first + it * LG::SLOTS + slot;
+        const bool valid = poly < npoly;
+        uint32_t lo = L.brl, so = G * L.brl;   // opaque per step (see k_ntt_fwd_large)
+        asm volatile("" : "+v"(lo), "+v"(so));
+        uint32_t r[32];
+        // pass-2 register j of lane l holds sub-block index brv5(j)*64 + l,
+        // i.e. global natural index G (brv5(j)*64 + l) + brv_g(B)
+        load32(r, in + (size_t)(valid ? poly : first) * N + kin + so, [](int j) { return G * 64 * brv5(j); });
+        inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        lds_p2_to_p1<P>(r, buf, L);
+        inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        const uint2 last = c_lastinv[LG::IDX][B];
+        inv_last_stage<P, false>(r, LG::PL::NINV, NINVP, last.x, last.y);   // [0,2q), scaled by n^-1
+        if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)
+            cross_gs<P>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)]);
+        constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1)
+        cross_gs<P>(r, buf, lds + (wave ^ D0) * XPOSE_WORDS, L.lane, (B & D0) != 0, c_cross[LG::IDX][1][1]);
+        if (valid) {
+            uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, csub<P::Q>(r[j]));
+        }
+    }
+}
+
+}  // namespace qntt

@@ -17,6 +17,8 @@
 
 namespace qntt {
 
+constexpr int NPARAM_SETS = 5;
+
 struct ParamSet {
     int id;
     uint32_t n, logn, q, psi;
@@ -40,12 +42,17 @@ inline uint32_t invmod(uint32_t a, uint32_t q) { return powmod(a, q - 2, q); }
 
 inline const ParamSet *param_set(int id)
 {
-    static const ParamSet sets[3] = {
+    // 3, 4: p-III's prime at n = 4096 / 8192 (q - 1 = 2^14 * 52255 admits
+    // negacyclic transforms up to n = 8192), for the multi-wave four-step
+    // kernels (ntt_large.hpp)
+    static const ParamSet sets[NPARAM_SETS] = {
         {0, 1024, 10, 8404993u, 2083362u, "ref(qTESLA-III-speed r1)"},
         {1, 1024, 10, 343576577u, powmod(3, (343576577u - 1) / 2048, 343576577u), "qTESLA-p-I"},
         {2, 2048, 11, 856145921u, powmod(3, (856145921u - 1) / 4096, 856145921u), "qTESLA-p-III"},
+        {3, 4096, 12, 856145921u, powmod(3, (856145921u - 1) / 8192, 856145921u), "p-III-q n=4096"},
+        {4, 8192, 13, 856145921u, powmod(3, (856145921u - 1) / 16384, 856145921u), "p-III-q n=8192"},
     };
-    return (id >= 0 && id < 3) ? &sets[id] : nullptr;
+    return (id >= 0 && id < NPARAM_SETS) ? &sets[id] : nullptr;
 }
 
 inline uint32_t bitrev(uint32_t j, uint32_t bits)

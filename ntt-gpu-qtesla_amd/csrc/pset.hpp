@@ -59,11 +59,15 @@ struct PSet {
 using PS0 = PSet<8404993u, 10, 2083362u>;
 using PS1 = PSet<343576577u, 10, cpow(3, (343576577u - 1) / 2048, 343576577u)>;
 using PS2 = PSet<856145921u, 11, cpow(3, (856145921u - 1) / 4096, 856145921u)>;
+using PS3 = PSet<856145921u, 12, cpow(3, (856145921u - 1) / 8192, 856145921u)>;
+using PS4 = PSet<856145921u, 13, cpow(3, (856145921u - 1) / 16384, 856145921u)>;
 static_assert(4ull * PS2::Q < (1ull << 32), "lazy bounds need 4q < 2^32");
 
 template <int PS> struct PSel;
 template <> struct PSel<0> { using T = PS0; };
 template <> struct PSel<1> { using T = PS1; };
 template <> struct PSel<2> { using T = PS2; };
+template <> struct PSel<3> { using T = PS3; };
+template <> struct PSel<4> { using T = PS4; };
 
 }  // namespace qntt

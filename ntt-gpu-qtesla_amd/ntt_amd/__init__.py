@@ -31,7 +31,7 @@ ROOT_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.environ.get("NTT_AMD_LIB") or os.path.join(ROOT_DIR, "lib", "libqtesla_ntt.so")
 HEADER_PATH = os.path.join(os.path.dirname(ROOT_DIR), "include", "qtesla_ntt.h")
 
-PARAM_SETS = {"ref": 0, "p-I": 1, "p-III": 2}
+PARAM_SETS = {"ref": 0, "p-I": 1, "p-III": 2, "p-III-4096": 3, "p-III-8192": 4}
 
 NTT_OK = 0
 NTT_ERR_PARAM = -1

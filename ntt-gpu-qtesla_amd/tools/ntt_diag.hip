@@ -142,8 +142,8 @@ extern "C" int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uin
     const uintptr_t a = (uintptr_t)d_in, b = (uintptr_t)d_out;
     if (a != b && a < b + bytes && b < a + bytes) return NTT_ERR_ALIAS;
     std::call_once(g_once, [] {
-        Tables tabs[3];
-        for (int i = 0; i < 3; i++) make_tables(*param_set(i), tabs[i]);
+        Tables tabs[NPARAM_SETS];
+        for (int i = 0; i < NPARAM_SETS; i++) make_tables(*param_set(i), tabs[i]);
         g_upload = upload_device_tables(tabs);
         int dev = 0;
         hipDeviceProp_t prop;

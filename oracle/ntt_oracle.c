@@ -39,6 +39,10 @@ int oracle_params_get(int ps, oracle_params *o)
         p.n = 1024; p.logn = 10; p.q = 343576577u; p.psi = powmod(3, (343576577u - 1) / 2048, 343576577u); break;
     case 2: /* qTESLA-p-III */
         p.n = 2048; p.logn = 11; p.q = 856145921u; p.psi = powmod(3, (856145921u - 1) / 4096, 856145921u); break;
+    case 3: /* p-III's prime at n = 4096 (larger n; not a qTESLA set) */
+        p.n = 4096; p.logn = 12; p.q = 856145921u; p.psi = powmod(3, (856145921u - 1) / 8192, 856145921u); break;
+    case 4: /* p-III's prime at n = 8192 (q - 1 = 2^14 * 52255) */
+        p.n = 8192; p.logn = 13; p.q = 856145921u; p.psi = powmod(3, (856145921u - 1) / 16384, 856145921u); break;
     default:
         return -1;
     }

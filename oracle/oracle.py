@@ -18,7 +18,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libntt_oracle.so")
 
-PARAM_SETS = {"ref": 0, "p-I": 1, "p-III": 2}
+PARAM_SETS = {"ref": 0, "p-I": 1, "p-III": 2, "p-III-4096": 3, "p-III-8192": 4}
 
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 _lib = None

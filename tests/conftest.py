@@ -9,6 +9,8 @@ for p in (os.path.join(ROOT, "ntt-gpu-qtesla_amd"), os.path.join(ROOT, "oracle")
         sys.path.insert(0, p)
 
 PARAM_SETS = ("ref", "p-I", "p-III")
+# p-III's prime at n = 4096 / 8192: the multi-wave four-step kernels (ntt_large.hpp)
+LARGE_SETS = ("p-III-4096", "p-III-8192")
 
 
 def pytest_configure(config):

@@ -22,7 +22,8 @@ def test_exports_every_declared_symbol(ntt):
 def test_error_codes_before_any_gpu_work(ntt):
     L = ntt.lib()
     fake = 0x10000  # never dereferenced: validation fails first
-    assert L.poly_ntt(fake, None, 1, 3, None) == ntt.NTT_ERR_PARAM
+    assert L.poly_ntt(fake, None, 1, 5, None) == ntt.NTT_ERR_PARAM
+    assert L.poly_mul(fake, fake, fake, 1, 3, None) == ntt.NTT_ERR_PARAM      # no fused product at n > 2048
     assert L.poly_ntt(None, None, 1, 0, None) == ntt.NTT_ERR_NULL
     assert L.poly_ntt(fake + 2, None, 1, 0, None) == ntt.NTT_ERR_ALIGN
     assert L.poly_ntt(None, None, 0, 0, None) == ntt.NTT_OK      # empty batch is a no-op
@@ -45,6 +46,8 @@ def test_param_info(ntt):
     assert ntt.param_info("ref")["q"] == 8404993
     assert ntt.param_info("p-I")["q"] == 343576577 and ntt.param_info("p-I")["n"] == 1024
     assert ntt.param_info("p-III")["q"] == 856145921 and ntt.param_info("p-III")["n"] == 2048
+    assert ntt.param_info("p-III-4096")["n"] == 4096 and ntt.param_info("p-III-8192")["n"] == 8192
+    assert ntt.param_info("p-III-8192")["q"] == 856145921
     assert "gfx950" in ntt.build_info()
     h = ntt.build_hash()
     assert len(h) == 16 and all(c in "0123456789abcdef" for c in h), h

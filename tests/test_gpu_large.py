@@ -1,0 +1,138 @@
+"""GPU parity of the n = 4096 / 8192 transforms (multi-wave four-step kernels,
+ntt_large.hpp) against the CPU oracle, bit-exact.
+
+The oracle at these sizes is pinned by tests/test_oracle_large.py (O(n^2)
+definition, round trip on the reference's operand pattern, all-ones KAT).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import LARGE_SETS
+
+pytestmark = pytest.mark.gpu
+
+
+def _u32(ntt, t):
+    return ntt.to_numpy_u32(t)
+
+
+def _dev(ntt, a, dev):
+    return ntt.from_numpy_u32(a, dev)
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+@pytest.mark.parametrize("batch", [1, 2, 3, 7, 64, 1001])
+def test_large_fwd_inv_random(ntt, oracle, dev, ps, batch):
+    x = oracle.fill_uniform(batch, ps, 0xA11CE + batch, 0)
+    t = _dev(ntt, x, dev)
+    ntt.poly_ntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), oracle.poly_ntt(x, ps))
+    ntt.poly_invntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), x)
+    Y = oracle.fill_uniform(batch, ps, 0xB0B + batch, 0)
+    t = _dev(ntt, Y, dev)
+    ntt.poly_invntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), oracle.poly_invntt(Y, ps))
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+def test_large_edge_values_and_lazy_inputs(ntt, oracle, dev, ps):
+    n, q = ntt.param_info(ps)["n"], ntt.param_info(ps)["q"]
+    cases = np.stack([np.zeros(n, np.uint32), np.full(n, q - 1, np.uint32),
+                      np.eye(1, n, 0, dtype=np.uint32)[0], np.eye(1, n, n - 1, dtype=np.uint32)[0],
+                      np.eye(1, n, n // 2, dtype=np.uint32)[0], (np.arange(n) % 2 * (q - 1)).astype(np.uint32)])
+    for fwd in (True, False):
+        t = _dev(ntt, cases, dev)
+        (ntt.poly_ntt if fwd else ntt.poly_invntt)(t, ps)
+        want = oracle.poly_ntt(cases, ps) if fwd else oracle.poly_invntt(cases, ps)
+        assert np.array_equal(_u32(ntt, t), want)
+    x = oracle.fill_uniform(3, ps, 77, 0)
+    xl = (x.astype(np.uint64) + q).astype(np.uint32)   # inputs in [q, 2q)
+    t = _dev(ntt, xl, dev)
+    ntt.poly_ntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), oracle.poly_ntt(x, ps))
+    t = _dev(ntt, xl, dev)
+    ntt.poly_invntt(t, ps)
+    assert np.array_equal(_u32(ntt, t), oracle.poly_invntt(x, ps))
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+def test_large_out_of_place_and_pattern(ntt, oracle, dev, ps):
+    n = ntt.param_info(ps)["n"]
+    pat = np.zeros((1, n), np.uint32)
+    pat[0, : n // 2] = n // 2 - np.arange(n // 2)   # init_operand (NTT.cu:10-15)
+    a = _dev(ntt, pat, dev)
+    b = torch.empty_like(a)
+    ntt.poly_ntt_oop(b, a, ps)
+    assert np.array_equal(_u32(ntt, a), pat)
+    assert np.array_equal(_u32(ntt, b), oracle.poly_ntt(pat, ps))
+    ntt.poly_invntt_oop(a, b, ps)
+    assert np.array_equal(_u32(ntt, a), pat)
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+def test_large_polymul_composition(ntt, oracle, dev, ps):
+    """INV(FWD(a) o FWD(b)) through poly_pointwise == the oracle product; the
+    all-ones KAT z[k] = 2k + 2 - n mod q (NTT.cu:2360, 2433-2438)."""
+    n, q = ntt.param_info(ps)["n"], ntt.param_info(ps)["q"]
+    a = oracle.fill_uniform(5, ps, 1, 0)
+    b = oracle.fill_uniform(5, ps, 2, 0)
+    a[4] = 1
+    b[4] = 1
+    ta, tb = _dev(ntt, a, dev), _dev(ntt, b, dev)
+    tc = torch.empty_like(ta)
+    ntt.poly_ntt(ta, ps)
+    ntt.poly_ntt(tb, ps)
+    ntt.poly_pointwise(tc, ta, tb, ps)
+    ntt.poly_invntt(tc, ps)
+    c = _u32(ntt, tc)
+    assert np.array_equal(c, oracle.poly_mul(a, b, ps))
+    assert np.array_equal(c[4], ((2 * np.arange(n) + 2 - n) % q).astype(np.uint32))
+
+
+def test_large_unsupported_ops(ntt, dev):
+    """Bit-reversed orders, the fused product and Nussbaumer exist for n <= 2048
+    only: NTT_ERR_PARAM, nothing launched."""
+    L = ntt.lib()
+    for ps in (3, 4):
+        n = ntt.param_info(ps)["n"]
+        t = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+        u = torch.zeros_like(t)
+        p, q = t.data_ptr(), u.data_ptr()
+        assert L.poly_ntt_bitrev(q, p, 2, ps, None) == ntt.NTT_ERR_PARAM
+        assert L.poly_invntt_bitrev(q, p, 2, ps, None) == ntt.NTT_ERR_PARAM
+        assert L.poly_bitrev_copy(q, p, 2, ps, None) == ntt.NTT_ERR_PARAM
+        assert L.poly_mul(q, p, p, 2, ps, None) == ntt.NTT_ERR_PARAM
+        assert L.poly_mul_ntt(q, p, p, 2, ps, None) == ntt.NTT_ERR_PARAM
+        assert L.poly_mul_nussbaumer(q, p, p, 2, ps, 0, None) == ntt.NTT_ERR_PARAM
+        assert L.poly_ntt(p, None, 0, ps, None) == 0
+    torch.cuda.synchronize()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("ps,batch", [("p-III-4096", 1 << 18), ("p-III-8192", (1 << 17) + 3)])
+def test_large_full_batch_properties(ntt, oracle, dev, ps, batch):
+    """4-GiB batches: round trip on device, sampled polys vs the oracle, linearity."""
+    n, q = ntt.param_info(ps)["n"], ntt.param_info(ps)["q"]
+    x = torch.empty(batch * n, dtype=torch.int32, device=dev)
+    ntt.fill_uniform(x, ps, 0x5EED0006, 0)
+    ref = x.clone()
+    ntt.poly_ntt(x, ps)
+    rng = np.random.default_rng(2)
+    idx = np.unique(np.concatenate([[0, batch - 1], rng.integers(0, batch, 62)]))
+    sel = torch.as_tensor(idx, device=dev)
+    assert np.array_equal(ntt.to_numpy_u32(x.view(batch, n)[sel]),
+                          oracle.poly_ntt(ntt.to_numpy_u32(ref.view(batch, n)[sel]), ps))
+    X = x.clone()
+    ntt.poly_invntt(x, ps)
+    assert torch.equal(x, ref)
+    # linearity: NTT(a) + NTT(b) == NTT(a + b mod q) on the whole batch
+    b = torch.empty_like(x)
+    ntt.fill_uniform(b, ps, 0x5EED0007, 0)
+    s = (((ref.to(torch.int64) & 0xFFFFFFFF) + (b.to(torch.int64) & 0xFFFFFFFF)) % q).to(torch.int32)
+    del ref, x
+    ntt.poly_ntt(b, ps)
+    ntt.poly_ntt(s, ps)
+    lhs = ((X.to(torch.int64) & 0xFFFFFFFF) + (b.to(torch.int64) & 0xFFFFFFFF)) % q
+    assert torch.equal(lhs, s.to(torch.int64) & 0xFFFFFFFF)
