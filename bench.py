@@ -190,7 +190,8 @@ def main():
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
                     help="BASELINE.json config (sets op / param / batch defaults)")
     ap.add_argument("--op", default=None, choices=OPS)
-    ap.add_argument("--param", default=None, choices=["ref", "p-I", "p-III"])
+    ap.add_argument("--param", default=None, choices=["ref", "p-I", "p-III", "p-III-4096", "p-III-8192"],
+                    help="p-III-4096 / p-III-8192: the n > 2048 four-step transforms (fwd / inv / fwdinv only)")
     ap.add_argument("--batch", type=int, default=None, help="polynomials per GPU")
     ap.add_argument("--ring", default=None, choices=["q", "m32"], help="--op nussbaumer: mod q or mod 2^32-1")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],

@@ -38,6 +38,13 @@ extern "C" {
 #define NTT_PARAM_REF 0   /* n = 1024, q = 8404993,   psi = 2083362          */
 #define NTT_PARAM_P_I 1   /* n = 1024, q = 343576577, psi = 3^((q-1)/2n)    */
 #define NTT_PARAM_P_III 2 /* n = 2048, q = 856145921, psi = 3^((q-1)/2n)    */
+/* Larger transforms over p-III's prime (q - 1 = 2^14 * 52255 admits
+ * negacyclic n up to 8192), for the reference's n > 2048 dataflows (its
+ * Stockham / CT2 kernels, NTT.cu:1085-1153, 1268-1337, 667-951): multi-wave
+ * four-step kernels.  poly_ntt / poly_invntt (and their _oop forms) only;
+ * every other entry point returns NTT_ERR_PARAM for these sets. */
+#define NTT_PARAM_N4096 3 /* n = 4096, q = 856145921, psi = 3^((q-1)/2n)    */
+#define NTT_PARAM_N8192 4 /* n = 8192, q = 856145921, psi = 3^((q-1)/2n)    */
 
 /* ---- error codes ------------------------------------------------------- */
 #define NTT_OK 0

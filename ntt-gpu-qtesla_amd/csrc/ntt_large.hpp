@@ -17,11 +17,16 @@
 //     the n = 2048 kernel's passes (register pass, permlane32 stage, LDS
 //     transpose, register pass) with per-wave twiddle tables;
 //   * natural-order output k' of sub-block B is global index G k' + brv_g(B):
-//     the G waves' stores interleave at a stride of G words.  They run
-//     together on one CU, so the partial lines merge in the L2.
-// The inverse runs in reverse: strided loads, the 2048-point GS passes with
-// T_B^-1 (n^-1 folded into their last stage), the g GS stages across waves
-// (LDS exchanges), contiguous stores.
+//     the G waves of a polynomial exchange their outputs through their LDS
+//     buffers (an all-to-all, conflict-free by a per-wave rotation, see
+//     xch_pos) so that each wave stores one contiguous 2048-word block.
+//     Storing the sub-blocks directly (stride G words) wrote 1.7x / 2.5x the
+//     algorithmic bytes at n = 4096 / 8192 (partial lines, WRITE_SIZE),
+//     profiles/r02/s4/large_pmc.txt.
+// The inverse runs in reverse: contiguous loads scattered to the owning
+// waves through LDS (strided loads fetched 1.3x / 1.7x), the 2048-point GS
+// passes with T_B^-1 (n^-1 folded into their last stage), the g GS stages
+// across waves (LDS exchanges), contiguous stores.
 #pragma once
 #include "ntt_device.hpp"
 
@@ -109,6 +114,16 @@ __device__ __forceinline__ void cross_gs(uint32_t (&r)[32], uint32_t *mine, cons
     __syncthreads();
 }
 
+// Position of sub-block output k' in its wave's 8 KiB exchange buffer: the
+// rotation by B 64/G words makes both sides conflict-free -- the owner
+// accesses 64 consecutive k' per instruction, and a contiguous run of 64
+// global words g = G k' + brv_g(B) hits (g / G) + B 64/G = 64 distinct banks.
+template <int G>
+__device__ __forceinline__ uint32_t xch_pos(uint32_t kp, uint32_t B)
+{
+    return (kp + B * (64u / G)) & 2047u;
+}
+
 // The workgroup's G lane-twiddle images of one direction (contiguous in
 // g_tw2imgL) into LDS after the transpose buffers.
 template <class LG, bool INV>
@@ -142,15 +157,14 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
     __syncthreads();
     const LT L;
     const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
-    const uint32_t kout = brv_g(B, LG::LOGG);   // global index = G k' + kout
 #pragma unroll 1
     for (uint32_t it = 0; it < steps; ++it) {
         const uint32_t poly = first + it * LG::SLOTS + slot;
         const bool valid = poly < npoly;
         // lane offsets opaque per step: the accesses keep the scalar base +
         // 32-bit offset form instead of loop-invariant 64-bit VGPR addresses
-        uint32_t lo = L.brl, so = G * L.brl;
-        asm volatile("" : "+v"(lo), "+v"(so));
+        uint32_t lo = L.brl;
+        asm volatile("" : "+v"(lo));
         uint32_t r[32];
         load32(r, in + (size_t)(valid ? poly : first) * N + B * 2048u + lo, [](int j) { return 64 * j; });
         // pos bit L-1 (k = 1), then for n = 8192 pos bit 11 (k = 2 + B/2)
@@ -162,10 +176,24 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
         fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), tw2 + TW2_ENTRIES * 64 + opaque_zero());
         lds_p1_to_p2<P>(r, buf, L);
         fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
-        if (valid) {
-            uint32_t *dst = out + (size_t)poly * N + kout + so;
+        // all-to-all through the exchange buffers: register j of lane l holds
+        // k' = brv5(j) 64 + l, global index G k' + brv_g(B); this wave then
+        // stores global words [2048 B, 2048 B + 2048), lane-contiguous runs
 #pragma unroll
-            for (int j = 0; j < 32; ++j) st_out(dst + G * 64 * brv5(j), canon4<P>(r[j]));
+        for (int j = 0; j < 32; ++j) buf[xch_pos<G>(brv5(j) * 64 + L.lane, B)] = canon4<P>(r[j]);
+        __syncthreads();
+        {
+            const uint32_t bs = brv_g(L.lane % G, LG::LOGG);   // source wave of global word g (g = lane mod G)
+            const uint32_t *src = lds + (slot * G + bs) * XPOSE_WORDS;
+            const uint32_t k0 = 2048u / G * B + L.lane / G;     // k' of j = 0
+#pragma unroll
+            for (int j = 0; j < 32; ++j) r[j] = src[xch_pos<G>(k0 + 64u / G * j, bs)];
+        }
+        __syncthreads();   // the buffers are free for the next step's exchanges
+        if (valid) {
+            uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, r[j]);
         }
     }
 }
@@ -190,17 +218,28 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
     __syncthreads();
     const LT L;
     const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
-    const uint32_t kin = brv_g(B, LG::LOGG);
 #pragma unroll 1
     for (uint32_t it = 0; it < steps; ++it) {
         const uint32_t poly = first + it * LG::SLOTS + slot;
         const bool valid = poly < npoly;
-        uint32_t lo = L.brl, so = G * L.brl;   // opaque per step (see k_ntt_fwd_large)
-        asm volatile("" : "+v"(lo), "+v"(so));
+        uint32_t lo = L.brl;   // opaque per step (see k_ntt_fwd_large)
+        asm volatile("" : "+v"(lo));
         uint32_t r[32];
-        // pass-2 register j of lane l holds sub-block index brv5(j)*64 + l,
-        // i.e. global natural index G (brv5(j)*64 + l) + brv_g(B)
-        load32(r, in + (size_t)(valid ? poly : first) * N + kin + so, [](int j) { return G * 64 * brv5(j); });
+        // contiguous load of global words [2048 B, 2048 B + 2048), scattered
+        // to the owning waves: global g = G k' + brv_g(B') belongs to wave B'
+        // (the previous step's last cross_gs barrier freed the buffers)
+        load32(r, in + (size_t)(valid ? poly : first) * N + B * 2048u + lo, [](int j) { return 64 * j; });
+        {
+            const uint32_t bt = brv_g(L.lane % G, LG::LOGG);   // owner of g (g = lane mod G)
+            uint32_t *dst = lds + (slot * G + bt) * XPOSE_WORDS;
+            const uint32_t k0 = 2048u / G * B + L.lane / G;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) dst[xch_pos<G>(k0 + 64u / G * j, bt)] = r[j];
+        }
+        __syncthreads();
+        // pass-2 register j of lane l holds sub-block index k' = brv5(j)*64 + l
+#pragma unroll
+        for (int j = 0; j < 32; ++j) r[j] = buf[xch_pos<G>(brv5(j) * 64 + L.lane, B)];
         inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
         lds_p2_to_p1<P>(r, buf, L);
         inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), tw2 + TW2_ENTRIES * 64 + opaque_zero());

@@ -19,6 +19,18 @@ def test_exports_every_declared_symbol(ntt):
         assert hasattr(L, f), f"{f} declared in qtesla_ntt.h but not exported"
 
 
+def test_header_param_sets_match_library(ntt):
+    """Every NTT_PARAM_* the header defines names a set the library knows, with
+    the n its comment states (param sets 3 / 4: the n = 4096 / 8192 transforms)."""
+    src = open(ntt.HEADER_PATH).read()
+    defs = re.findall(r"#define NTT_PARAM_(\w+) (\d+)\s*/\*\s*n = (\d+), q = (\d+)", src)
+    assert len(defs) == len(ntt.PARAM_SETS), defs
+    by_id = {v: k for k, v in ntt.PARAM_SETS.items()}
+    for _, ps, n, q in defs:
+        info = ntt.param_info(by_id[int(ps)])
+        assert (info["n"], info["q"]) == (int(n), int(q))
+
+
 def test_error_codes_before_any_gpu_work(ntt):
     L = ntt.lib()
     fake = 0x10000  # never dereferenced: validation fails first
