@@ -115,13 +115,14 @@ __device__ __forceinline__ void cross_gs(uint32_t (&r)[32], uint32_t *mine, cons
 }
 
 // Position of sub-block output k' in its wave's 8 KiB exchange buffer: the
-// rotation by B 64/G words makes both sides conflict-free -- the owner
-// accesses 64 consecutive k' per instruction, and a contiguous run of 64
-// global words g = G k' + brv_g(B) hits (g / G) + B 64/G = 64 distinct banks.
+// rotation by B 32/G words makes both sides conflict-free (ds_*_b32 runs as
+// two 32-lane groups, bank = dword mod 32) -- the owner accesses consecutive
+// k' per instruction, and 32 consecutive global words g = G k' + brv_g(B)
+// hit banks (g / G) + B 32/G: 32 distinct (tests/test_lds_layout.py).
 template <int G>
 __device__ __forceinline__ uint32_t xch_pos(uint32_t kp, uint32_t B)
 {
-    return (kp + B * (64u / G)) & 2047u;
+    return (kp + B * (32u / G)) & 2047u;
 }
 
 // The workgroup's G lane-twiddle images of one direction (contiguous in

@@ -123,3 +123,43 @@ def test_bitreversed_side_is_lane_contiguous(logn):
             pos = 32 * L.Lp + j
             assert brv(pos, logn) == brv(j, 5) * S + L.brl
             assert L.brl == (lane if logn == 11 else lane & 31)
+
+
+# ---------------------------------------------------------------------------
+# n = 4096 / 8192 all-to-all exchange (ntt_large.hpp, xch_pos): G waves per
+# polynomial, wave B holds sub-block outputs k' (global index G k' + brv_G(B))
+# in the pass-2 arrangement; each wave stores / loads one contiguous block.
+# ---------------------------------------------------------------------------
+def brv5(j):
+    return brv(j, 5)
+
+
+def xch_pos(kp, B, G):
+    return (kp + B * (32 // G)) & 2047
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_large_exchange_mapping_and_banks(G):
+    logg = G.bit_length() - 1
+    # owner side: register j of lane l holds k' = brv5(j)*64 + l
+    for B in range(G):
+        pos = {xch_pos(brv5(j) * 64 + l, B, G) for j in range(32) for l in range(64)}
+        assert pos == set(range(2048)), "rotation is a bijection of the 8 KiB buffer"
+        for j in range(32):
+            for half in (range(32), range(32, 64)):
+                banks = [xch_pos(brv5(j) * 64 + l, B, G) % 32 for l in half]
+                assert len(set(banks)) == 32
+    # other side (fwd gather / inv scatter): wave Bw, load/store j, lane l
+    # touches global word g = 2048 Bw + 64 j + l, held by wave bs at k' = g // G
+    for Bw in range(G):
+        for j in range(32):
+            for half in (range(32), range(32, 64)):
+                addr = []
+                for l in half:
+                    g = 2048 * Bw + 64 * j + l
+                    bs = brv(l % G, logg)
+                    k0 = 2048 // G * Bw + l // G
+                    kp = k0 + 64 // G * j
+                    assert G * kp + brv(bs, logg) == g, "the word read is global index g"
+                    addr.append(bs * 2048 + xch_pos(kp, bs, G))
+                assert len({a % 32 for a in addr}) == 32, (G, Bw, j)
