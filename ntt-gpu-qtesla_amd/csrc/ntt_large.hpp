@@ -22,7 +22,8 @@
 //     xch_pos) so that each wave stores one contiguous 2048-word block.
 //     Storing the sub-blocks directly (stride G words) wrote 1.7x / 2.5x the
 //     algorithmic bytes at n = 4096 / 8192 (partial lines, WRITE_SIZE),
-//     profiles/r02/s4/large_pmc.txt.
+//     profiles/r02/s4/large_pmc.txt;
+//   * every exchange synchronises only the G waves of its polynomial (SlotSync).
 // The inverse runs in reverse: contiguous loads scattered to the owning
 // waves through LDS (strided loads fetched 1.3x / 1.7x), the 2048-point GS
 // passes with T_B^-1 (n^-1 folded into their last stage), the g GS stages
@@ -59,11 +60,45 @@ struct Large {
     static constexpr int SLOTS = WAVES / G;   // polynomials per workgroup step
     static constexpr int NT = WAVES * 64;
     static constexpr int IDX = PS - LARGE_PS0;
-    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + G * TW2_WORDS;
+    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + G * TW2_WORDS + SLOTS;   // + slot counters
 };
 
 // global-order offset of sub-block B's outputs: brv_g(B)
 __host__ __device__ constexpr uint32_t brv_g(uint32_t b, int logg) { return logg == 1 ? b : (((b & 1u) << 1) | (b >> 1)); }
+
+// Barrier among the G waves of one polynomial slot (the workgroup holds
+// WAVES/G slots).  A workgroup-wide s_barrier would keep all 16 / 12 waves
+// in lock step, so every wave of the CU would load, compute and store in the
+// same phase; the slot barrier lets the slots drift apart.  Monotonic LDS
+// counter per slot: each wave adds 1 (release) and waits (acquire) until
+// the slot's G arrivals of this barrier are in.  Measured: n=4096 fwd 5.07
+// -> 3.87 ms, n=8192 fwd 5.53 -> 4.71 ms against __syncthreads
+// (profiles/r02/s4/large/ab_slotsync_*.log).  The wait is bounded (2^22
+// short sleeps, ~0.1 s, far beyond any legitimate wait on partners resident
+// on the same CU) so that a broken schedule could never hang the GPU.
+#ifndef LARGE_SLOT_SYNC
+#define LARGE_SLOT_SYNC 1
+#endif
+struct SlotSync {
+    uint32_t *ctr;
+    uint32_t target;
+    template <int G>
+    __device__ __forceinline__ void wait()
+    {
+#if LARGE_SLOT_SYNC
+        target += G;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
+            if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
+        __syncthreads();
+#endif
+    }
+};
 
 // One radix-2 CT stage across waves: this wave and its partner hold the two
 // halves at the same register/lane slots; `hi` = this wave holds the upper
@@ -71,9 +106,9 @@ __host__ __device__ constexpr uint32_t brv_g(uint32_t b, int logg) { return logg
 // sends tn = -(w y mod q); lo keeps a + t, hi keeps a - t + 2q, in [0,4q).
 // Exchange through the waves' own transpose buffers, layout [j][lane]
 // (conflict-free b32 accesses); the second barrier frees the buffers.
-template <class P, bool RED>
+template <class P, bool RED, int G>
 __device__ __forceinline__ void cross_ct(uint32_t (&r)[32], uint32_t *mine, const uint32_t *theirs, uint32_t lane, bool hi,
-                                         uint2 w)
+                                         uint2 w, SlotSync &ss)
 {
     if (hi) {
 #pragma unroll
@@ -84,7 +119,7 @@ __device__ __forceinline__ void cross_ct(uint32_t (&r)[32], uint32_t *mine, cons
     }
 #pragma unroll
     for (int j = 0; j < 32; ++j) mine[j * 64 + lane] = r[j];
-    __syncthreads();
+    ss.wait<G>();
     if (hi) {
 #pragma unroll
         for (int j = 0; j < 32; ++j) r[j] = theirs[j * 64 + lane] + r[j] + 2 * P::Q;
@@ -92,18 +127,18 @@ __device__ __forceinline__ void cross_ct(uint32_t (&r)[32], uint32_t *mine, cons
 #pragma unroll
         for (int j = 0; j < 32; ++j) r[j] = r[j] - theirs[j * 64 + lane];
     }
-    __syncthreads();
+    ss.wait<G>();
 }
 
 // One GS stage across waves, inputs and outputs in [0,2q): lo keeps
 // (x + y) mod 2q, hi keeps (x - y) w by the signed Shoup product.
-template <class P>
+template <class P, int G>
 __device__ __forceinline__ void cross_gs(uint32_t (&r)[32], uint32_t *mine, const uint32_t *theirs, uint32_t lane, bool hi,
-                                         uint2 w)
+                                         uint2 w, SlotSync &ss)
 {
 #pragma unroll
     for (int j = 0; j < 32; ++j) mine[j * 64 + lane] = r[j];
-    __syncthreads();
+    ss.wait<G>();
     if (hi) {
 #pragma unroll
         for (int j = 0; j < 32; ++j) r[j] = sshoup_mul<P::Q>(theirs[j * 64 + lane] - r[j], w.x, w.y);
@@ -111,7 +146,7 @@ __device__ __forceinline__ void cross_gs(uint32_t (&r)[32], uint32_t *mine, cons
 #pragma unroll
         for (int j = 0; j < 32; ++j) r[j] = csub<P::Q2>(r[j] + theirs[j * 64 + lane]);
     }
-    __syncthreads();
+    ss.wait<G>();
 }
 
 // Position of sub-block output k' in its wave's 8 KiB exchange buffer: the
@@ -155,7 +190,10 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
     uint32_t *const buf = lds + wave * XPOSE_WORDS;
     const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + B * TW2_WORDS);
     fill_large_tw<LG, false>(lds);
+    uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + G * TW2_WORDS;
+    if (threadIdx.x < (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;
     __syncthreads();
+    SlotSync ss{ctrs + slot, 0};
     const LT L;
     const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
 #pragma unroll 1
@@ -170,10 +208,10 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
         load32(r, in + (size_t)(valid ? poly : first) * N + B * 2048u + lo, [](int j) { return 64 * j; });
         // pos bit L-1 (k = 1), then for n = 8192 pos bit 11 (k = 2 + B/2)
         constexpr uint32_t D0 = G / 2;
-        cross_ct<P, false>(r, buf, lds + (wave ^ D0) * XPOSE_WORDS, L.lane, (B & D0) != 0, c_cross[LG::IDX][0][1]);
+        cross_ct<P, false, G>(r, buf, lds + (wave ^ D0) * XPOSE_WORDS, L.lane, (B & D0) != 0, c_cross[LG::IDX][0][1], ss);
         if constexpr (G == 4)
-            cross_ct<P, true>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0,
-                              c_cross[LG::IDX][0][2 + (B >> 1)]);
+            cross_ct<P, true, G>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0,
+                                 c_cross[LG::IDX][0][2 + (B >> 1)], ss);
         fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), tw2 + TW2_ENTRIES * 64 + opaque_zero());
         lds_p1_to_p2<P>(r, buf, L);
         fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
@@ -182,7 +220,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
         // stores global words [2048 B, 2048 B + 2048), lane-contiguous runs
 #pragma unroll
         for (int j = 0; j < 32; ++j) buf[xch_pos<G>(brv5(j) * 64 + L.lane, B)] = canon4<P>(r[j]);
-        __syncthreads();
+        ss.wait<G>();
         {
             const uint32_t bs = brv_g(L.lane % G, LG::LOGG);   // source wave of global word g (g = lane mod G)
             const uint32_t *src = lds + (slot * G + bs) * XPOSE_WORDS;
@@ -190,7 +228,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
 #pragma unroll
             for (int j = 0; j < 32; ++j) r[j] = src[xch_pos<G>(k0 + 64u / G * j, bs)];
         }
-        __syncthreads();   // the buffers are free for the next step's exchanges
+        ss.wait<G>();   // the buffers are free for the next step's exchanges
         if (valid) {
             uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
 #pragma unroll
@@ -216,7 +254,10 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
     uint32_t *const buf = lds + wave * XPOSE_WORDS;
     const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + B * TW2_WORDS);
     fill_large_tw<LG, true>(lds);
+    uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + G * TW2_WORDS;
+    if (threadIdx.x < (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;
     __syncthreads();
+    SlotSync ss{ctrs + slot, 0};
     const LT L;
     const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
 #pragma unroll 1
@@ -237,7 +278,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
 #pragma unroll
             for (int j = 0; j < 32; ++j) dst[xch_pos<G>(k0 + 64u / G * j, bt)] = r[j];
         }
-        __syncthreads();
+        ss.wait<G>();
         // pass-2 register j of lane l holds sub-block index k' = brv5(j)*64 + l
 #pragma unroll
         for (int j = 0; j < 32; ++j) r[j] = buf[xch_pos<G>(brv5(j) * 64 + L.lane, B)];
@@ -247,9 +288,9 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
         const uint2 last = c_lastinv[LG::IDX][B];
         inv_last_stage<P, false>(r, LG::PL::NINV, NINVP, last.x, last.y);   // [0,2q), scaled by n^-1
         if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)
-            cross_gs<P>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)]);
+            cross_gs<P, G>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)], ss);
         constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1)
-        cross_gs<P>(r, buf, lds + (wave ^ D0) * XPOSE_WORDS, L.lane, (B & D0) != 0, c_cross[LG::IDX][1][1]);
+        cross_gs<P, G>(r, buf, lds + (wave ^ D0) * XPOSE_WORDS, L.lane, (B & D0) != 0, c_cross[LG::IDX][1][1], ss);
         if (valid) {
             uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
 #pragma unroll
