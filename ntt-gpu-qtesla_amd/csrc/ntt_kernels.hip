@@ -85,7 +85,7 @@ int device_ready(DevInfo **out)
 // grows with the batch (amortising the 16 KiB LDS-table prologue) but never
 // beyond what keeps >= NTT_MIN_WG_PER_CU workgroups per CU in flight.
 #ifndef NTT_MIN_WG_PER_CU
-#define NTT_MIN_WG_PER_CU 2   // 4 and 8 measured 2-5 % slower on a 65 536-poly n=1024 launch, equal at 2^20 (profiles/r01/ab_launch_shape.json)
+#define NTT_MIN_WG_PER_CU 4   // ppw 4 instead of 8 at 65 536 n=1024 polys: 3-4 % faster (profiles/r02/s4/ab_launch_ppw_p1_65536.log); 2^20 keeps ppw 16
 #endif
 #ifndef NTT_PPW_MAX
 #define NTT_PPW_MAX 16

@@ -68,7 +68,10 @@ constexpr int NUS_WAVES = NUS_WG / 64;
 constexpr int NUS_PAIRS = NUS_WAVES / 2;
 constexpr int NUS_MAT_WORDS = 4096;             // one 64-row x R x H matrix (16 KiB)
 constexpr int NUS_PAIR_WORDS = 2 * NUS_MAT_WORDS;
-constexpr int NUS_PPW_MAX = 16;
+#ifndef NUS_PPW_CFG
+#define NUS_PPW_CFG 1   // one unit per workgroup (no table prologue to amortise): 2 % faster than 16, profiles/r02/s4/ab_nussbaumer_ppw.log
+#endif
+constexpr int NUS_PPW_MAX = NUS_PPW_CFG;
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F &&f)
