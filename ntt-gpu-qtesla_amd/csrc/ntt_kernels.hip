@@ -366,6 +366,18 @@ int ntt_fill_uniform(uint32_t *d_poly, size_t batch, int ps, uint64_t seed, uint
 
 int ntt_last_hip_error(void) { return t_last_hip; }
 
+int ntt_sync_expiries(uint32_t *count)
+{
+    if (!count) return NTT_ERR_NULL;
+    const hipError_t e = hipMemcpyFromSymbol(count, HIP_SYMBOL(g_slot_sync_expired), sizeof(uint32_t), 0,
+                                             hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        t_last_hip = (int)e;
+        return NTT_ERR_HIP;
+    }
+    return NTT_OK;
+}
+
 
 
 const char *ntt_strerror(int code)

@@ -79,6 +79,9 @@ __host__ __device__ constexpr uint32_t brv_g(uint32_t b, int logg) { return logg
 #ifndef LARGE_SLOT_SYNC
 #define LARGE_SLOT_SYNC 1
 #endif
+// count of slot-barrier waits that hit the bound (ntt_sync_expiries): 0 unless
+// the schedule broke; a launch that adds to it produced invalid results
+__device__ unsigned int g_slot_sync_expired;
 struct SlotSync {
     uint32_t *ctr;
     uint32_t target;
@@ -89,10 +92,15 @@ struct SlotSync {
         target += G;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        bool arrived = false;
         for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
-            if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+            if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
+                arrived = true;
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
         }
+        if (!arrived && (threadIdx.x & 63) == 0) atomicAdd(&g_slot_sync_expired, 1u);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #else
         __syncthreads();

@@ -90,6 +90,7 @@ def lib():
         L.ntt_strerror.restype = ctypes.c_char_p
         L.ntt_strerror.argtypes = [ctypes.c_int]
         L.ntt_build_info.argtypes = [ctypes.c_char_p, _sz]
+        L.ntt_sync_expiries.argtypes = [_u32p]
         L.ntt_host_ctx_create.argtypes = [ctypes.POINTER(_vp), ctypes.c_int, _sz, ctypes.c_int]
         L.ntt_host_ctx_destroy.argtypes = [_vp]
         for nm in ("poly_ntt_host", "poly_invntt_host"):
@@ -123,6 +124,14 @@ def tables(param_set) -> dict:
     out = {k: np.zeros(n, np.uint32) for k in names}
     _check(lib().ntt_get_tables(_ps(param_set), *(out[k].ctypes.data_as(_u32p) for k in names)), "ntt_get_tables")
     return out
+
+
+def sync_expiries() -> int:
+    """Expired bounded waits of the n = 4096 / 8192 kernels on the current
+    device (0 unless a per-polynomial barrier broke; see qtesla_ntt.h)."""
+    v = ctypes.c_uint32()
+    _check(lib().ntt_sync_expiries(ctypes.byref(v)), "ntt_sync_expiries")
+    return v.value
 
 
 def build_info() -> str:

@@ -136,3 +136,19 @@ def test_large_full_batch_properties(ntt, oracle, dev, ps, batch):
     ntt.poly_ntt(s, ps)
     lhs = ((X.to(torch.int64) & 0xFFFFFFFF) + (b.to(torch.int64) & 0xFFFFFFFF)) % q
     assert torch.equal(lhs, s.to(torch.int64) & 0xFFFFFFFF)
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+def test_large_slot_barriers_never_expire(ntt, oracle, dev, ps):
+    """The per-polynomial barriers' bounded waits (SlotSync) never run out,
+    over partial and full workgroups, in place and out of place."""
+    n = ntt.param_info(ps)["n"]
+    for batch in (5, 4099):
+        x = torch.empty(batch * n, dtype=torch.int32, device=dev)
+        ntt.fill_uniform(x, ps, 0x5107 + batch, 0)
+        ref = x.clone()
+        ntt.poly_ntt(x, ps)
+        ntt.poly_invntt(x, ps)
+        assert torch.equal(x, ref)
+    torch.cuda.synchronize()
+    assert ntt.sync_expiries() == 0
