@@ -30,10 +30,11 @@
 //   16 KiB of LDS and <= 256 VGPRs per wave -> 8 waves (2 per SIMD) per CU,
 //   one pair per workgroup.
 //   deferred     the reference halves after every inverse butterfly (moddiv2,
-//   scaling      NTT.cu:255-258); here all 2^-L is applied once to `a` on load:
-//                a 32-bit rotate in Z/(2^32-1) (2^32 == 1), a Shoup multiply
-//                by 2^(32-L) mod q in Z/q (the 2^32 cancels the Montgomery REDC
-//                of the inner products).
+//   scaling      NTT.cu:255-258); here all 2^-L is applied once: a 32-bit
+//                rotate of `a` on load in Z/(2^32-1) (2^32 == 1); in Z/q a
+//                signed Shoup multiply of the n OUTPUTS by 2^(32-L) mod q (the
+//                2^32 cancels the Montgomery REDC of the inner products), which
+//                also replaces the output's reduction.
 //
 // Z/q arithmetic is signed and lazy: values are int32 residues congruent mod q
 // with a compile-time magnitude bound; an add or sub is ONE instruction, and a
@@ -160,6 +161,11 @@ struct Ring<NTT_RING_M32, P> {
     static __device__ __forceinline__ uint32_t in_b(uint32_t x) { return x; }
     template <int B>
     static __device__ __forceinline__ uint32_t out(uint32_t x) { return x == 0xFFFFFFFFu ? 0u : x; }
+    // the deferred 2^-L is a rotate here: applied to a on load
+    template <int L>
+    static __device__ __forceinline__ uint32_t in_x(uint32_t x) { return in_a<L>(x); }
+    template <int L, int B>
+    static __device__ __forceinline__ uint32_t out_s(uint32_t x) { return out<B>(x); }
     static constexpr bool mul_ok(int, int) { return true; }
     static constexpr int mul_out(int, int) { return 0; }
     // negacyclic length-8 product; the 64-bit accumulator is folded after every
@@ -223,6 +229,22 @@ struct Ring<NTT_RING_Q, P> {
     {
         if constexpr (B > RB) x = red(x);
         return umin32(x, x + Q);   // (-q, q) -> [0, q)
+    }
+    // a enters like b; the deferred 2^-L (times the 2^32 that cancels the
+    // inner REDCs) is applied to the n outputs instead of the n inputs of a:
+    // a signed Shoup product by S = 2^(32-L) mod q (any int32 x, centred
+    // twiddle, quotient estimate minus one: result in (0, 2q)) that also
+    // replaces the output's reduction, then one conditional subtraction
+    template <int L>
+    static __device__ __forceinline__ uint32_t in_x(uint32_t x) { return in_b(x); }
+    template <int L, int B>
+    static __device__ __forceinline__ uint32_t out_s(uint32_t x)
+    {
+        constexpr uint32_t S = (uint32_t)((uint64_t)cpow(2, 32 - L, Q) % Q);
+        constexpr TwPair C = csigned_tw(S, Q);
+        const uint32_t e = (uint32_t)(((int64_t)(int32_t)x * (int32_t)C.y - 0x80000000ll) >> 32);
+        const uint32_t t = (uint32_t)((uint64_t)e * (0u - Q) + x * C.x);
+        return umin32(t, t - Q);
     }
     // products of bounds Bu, Bv: 8 terms must fit a signed 64-bit accumulator
     static constexpr bool mul_ok(int bu, int bv)
@@ -511,10 +533,10 @@ __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, u
         for (int q4 = 0; q4 < 8; ++q4) {
             const uint4 x = *(const uint4 *)(a + loff + 4 * q4);
             const uint4 y = *(const uint4 *)(b + loff + 4 * q4);
-            X[4 * q4 + 0] = RG::template in_a<G::L>(x.x);
-            X[4 * q4 + 1] = RG::template in_a<G::L>(x.y);
-            X[4 * q4 + 2] = RG::template in_a<G::L>(x.z);
-            X[4 * q4 + 3] = RG::template in_a<G::L>(x.w);
+            X[4 * q4 + 0] = RG::template in_x<G::L>(x.x);
+            X[4 * q4 + 1] = RG::template in_x<G::L>(x.y);
+            X[4 * q4 + 2] = RG::template in_x<G::L>(x.z);
+            X[4 * q4 + 3] = RG::template in_x<G::L>(x.w);
             Y[4 * q4 + 0] = RG::in_b(y.x);
             Y[4 * q4 + 1] = RG::in_b(y.y);
             Y[4 * q4 + 2] = RG::in_b(y.z);
@@ -614,7 +636,7 @@ __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, u
             A = RG::red(A);
             B = RG::red(B);
         }
-        o[t] = RG::template out<stage_out<RG>(BA)>(RG::add(A, RG::negm(bperm(addr1, B), mask1)));
+        o[t] = RG::template out_s<G::L, stage_out<RG>(BA)>(RG::add(A, RG::negm(bperm(addr1, B), mask1)));
     }
     if (valid) {   // both halves of a lane group share validity, so bpermute sources are valid lanes
         uint32_t *dst = c + (size_t)poly * P::N + 32u * ca + 16 * W;
