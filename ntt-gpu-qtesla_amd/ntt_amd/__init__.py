@@ -112,14 +112,32 @@ def _check(rc: int, where: str):
         raise NTTError(rc, where)
 
 
+_PARAM_CACHE: dict = {}
+_N_CACHE: dict = {}
+
+
+def _n(param_set) -> int:
+    """n of a parameter set, cached (the per-call wrappers' fast path)."""
+    n = _N_CACHE.get(param_set)
+    if n is None:
+        n = _N_CACHE[param_set] = param_info(param_set)["n"]
+    return n
+
+
 def param_info(param_set) -> dict:
-    vals = [ctypes.c_uint32() for _ in range(6)]
-    _check(lib().ntt_param_info(_ps(param_set), *[ctypes.byref(v) for v in vals]), "ntt_param_info")
-    return dict(zip(("n", "q", "psi", "omega", "omega_inv", "n_inv"), (v.value for v in vals)))
+    """n, q, psi, omega, omega^-1, n^-1 of a parameter set (immutable: cached,
+    so that the per-call wrappers cost no extra library call)."""
+    ps = _ps(param_set)
+    info = _PARAM_CACHE.get(ps)
+    if info is None:
+        vals = [ctypes.c_uint32() for _ in range(6)]
+        _check(lib().ntt_param_info(ps, *[ctypes.byref(v) for v in vals]), "ntt_param_info")
+        info = _PARAM_CACHE[ps] = dict(zip(("n", "q", "psi", "omega", "omega_inv", "n_inv"), (v.value for v in vals)))
+    return dict(info)
 
 
 def tables(param_set) -> dict:
-    n = param_info(param_set)["n"]
+    n = _n(param_set)
     names = ("bitrev_tbl", "Phi", "invPhi", "tf0", "ti0")
     out = {k: np.zeros(n, np.uint32) for k in names}
     _check(lib().ntt_get_tables(_ps(param_set), *(out[k].ctypes.data_as(_u32p) for k in names)), "ntt_get_tables")
@@ -205,6 +223,9 @@ def _run(where: str, tensors, stream, call):
     """Check the operands, make their device current and call `call(stream)`."""
     dev = _device_of(*tensors)
     torch = _torch()
+    if torch.cuda.current_device() == dev.index:   # already current: no device switch
+        _check(call(_stream(stream, dev)), where)
+        return
     with torch.cuda.device(dev):
         _check(call(_stream(stream, dev)), where)
 
@@ -219,7 +240,7 @@ def _same_batch(n: int, first, *others) -> int:
 
 def poly_ntt(t, param_set, stream=None):
     """In-place forward negacyclic NTT of a [batch, n] device tensor."""
-    n = param_info(param_set)["n"]
+    n = _n(param_set)
     b = _batch(t, n)
     _run("poly_ntt", (t,), stream, lambda s: lib().poly_ntt(t.data_ptr(), None, b, _ps(param_set), s))
     return t
@@ -227,14 +248,14 @@ def poly_ntt(t, param_set, stream=None):
 
 def poly_invntt(t, param_set, stream=None):
     """In-place inverse negacyclic NTT (includes n^-1 and psi^-i)."""
-    n = param_info(param_set)["n"]
+    n = _n(param_set)
     b = _batch(t, n)
     _run("poly_invntt", (t,), stream, lambda s: lib().poly_invntt(t.data_ptr(), None, b, _ps(param_set), s))
     return t
 
 
 def _oop(name, out, inp, param_set, stream):
-    n = param_info(param_set)["n"]
+    n = _n(param_set)
     b = _same_batch(n, inp, out)
     fn = getattr(lib(), name)
     _run(name, (out, inp), stream, lambda s: fn(out.data_ptr(), inp.data_ptr(), b, _ps(param_set), s))
@@ -265,7 +286,7 @@ def poly_bitrev_copy(out, inp, param_set, stream=None):
 
 
 def _mul(name, c, a, b, param_set, stream, *extra):
-    n = param_info(param_set)["n"]
+    n = _n(param_set)
     nb = _same_batch(n, a, b, c)
     fn = getattr(lib(), name)
     _run(name, (c, a, b), stream,
@@ -298,7 +319,7 @@ def poly_pointwise(c, a, b, param_set, stream=None):
 
 def fill_uniform(t, param_set, seed: int, first_poly: int = 0, stream=None):
     """Device-side counter-based uniform coefficients in [0, q)."""
-    n = param_info(param_set)["n"]
+    n = _n(param_set)
     b = _batch(t, n)
     _run("ntt_fill_uniform", (t,), stream,
          lambda s: lib().ntt_fill_uniform(t.data_ptr(), b, _ps(param_set), seed & (2**64 - 1), first_poly, s))
@@ -324,7 +345,7 @@ class HostContext:
 
     def __init__(self, param_set, chunk_polys: int = 0, nslots: int = 0):
         self.param_set = param_set
-        self.n = param_info(param_set)["n"]
+        self.n = _n(param_set)
         h = _vp()
         _check(lib().ntt_host_ctx_create(ctypes.byref(h), _ps(param_set), chunk_polys, nslots),
                "ntt_host_ctx_create")
