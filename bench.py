@@ -19,8 +19,9 @@ A step = one pass of the configured operation over the rank's whole batch
 as the reference's kernels).  Polynomials are independent, so the batch
 shards with no data-path collective: rank r owns polys [r*B, (r+1)*B) of one
 global counter-based input stream ("weak" scaling).  torch.distributed
-(RCCL, or gloo with --dist-backend gloo) is used only for the barrier and the
-max-over-ranks time.  Rank 0 prints ONE JSON line.
+(gloo by default: CPU tensors, no GPU collective on the path; RCCL with
+--dist-backend nccl) is used only for the barrier and the max / min over
+ranks of the timed region.  Rank 0 prints ONE JSON line.
 
 Roofline: the dominant kernel's average launch duration is measured with HIP
 events on the stream the kernels run on; achieved = algorithmic bytes per
@@ -96,14 +97,20 @@ class Dist:
             else:
                 dist.barrier()
 
-    def max(self, value: float) -> float:
+    def _reduce(self, value: float, op: str) -> float:
         if self.world <= 1:
             return value
         import torch
         import torch.distributed as dist
         t = torch.tensor([value], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN)
         return float(t.item())
+
+    def max(self, value: float) -> float:
+        return self._reduce(value, "max")
+
+    def min(self, value: float) -> float:
+        return self._reduce(value, "min")
 
     def close(self):
         if self.world > 1:
@@ -194,8 +201,9 @@ def main():
                     help="p-III-4096 / p-III-8192: the n > 2048 four-step transforms (fwd / inv / fwdinv only)")
     ap.add_argument("--batch", type=int, default=None, help="polynomials per GPU")
     ap.add_argument("--ring", default=None, choices=["q", "m32"], help="--op nussbaumer: mod q or mod 2^32-1")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="process group for the barrier / max-over-ranks (no data-path collective)")
+    ap.add_argument("--dist-backend", default="gloo", choices=["gloo", "nccl"],
+                    help="process group for the barrier / max-over-ranks only (no data-path collective, so "
+                         "gloo on CPU tensors by default; nccl = RCCL)")
     ap.add_argument("--pageable", action="store_true", help="*_host ops: pageable instead of pinned host buffers")
     ap.add_argument("--chunk", type=int, default=0, help="*_host ops: polys per chunk (0 = library default)")
     ap.add_argument("--slots", type=int, default=0, help="*_host ops: buffer slots (0 = library default)")
@@ -271,6 +279,13 @@ def main():
     t1 = time.perf_counter()
     dist.barrier()
     elapsed = dist.max(t1 - t0)
+    fastest = dist.min(t1 - t0)
+    expiries = None
+    if args.param in ("p-III-4096", "p-III-8192"):
+        # the n > 2048 kernels' slot barriers: an expired wait poisons its
+        # polynomial (sentinel output) and counts here; any count fails the run
+        torch.cuda.synchronize(device)
+        expiries = ntt_amd.sync_expiries()
 
     per_kind = {k: sum(evs[s][i][0].elapsed_time(evs[s][i][1]) for s in range(args.steps)) / args.steps
                 for i, k in enumerate(kinds)}  # ms per launch
@@ -284,7 +299,11 @@ def main():
         check = checker_legs(args, ntt_amd, torch, x, y, z, first, count, n)
         bad = 0.0 if all(v is None or v is True or (isinstance(v, dict) and v.get("ok")) for v in check.values()) \
             else 1.0
+        if expiries:
+            bad = 1.0
         check["all_ranks_ok"] = dist.max(bad) == 0.0
+    if expiries is not None:
+        check["slot_sync_expiries"] = expiries
 
     units = world * count * args.steps
     value = units / elapsed
@@ -301,6 +320,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "rank_ms_per_step": {"max": elapsed / args.steps * 1e3, "min": fastest / args.steps * 1e3},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -324,13 +344,25 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.close()
-    if not args.no_check and not check.get("all_ranks_ok", True):
+    if (not args.no_check and not check.get("all_ranks_ok", True)) or expiries:
         sys.exit(1)
+
+
+def host_threads():
+    """Threads for the batch-parallel CPU leg and why: the box's CPU share
+    (OMP_NUM_THREADS, which the GPU pool sets to the share of one GPU),
+    else the CPUs this process may run on."""
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env), visible, f"OMP_NUM_THREADS={env} (this box's CPU share per GPU); {visible} CPUs visible"
+    return visible, visible, f"all {visible} CPUs in this process's affinity mask"
 
 
 def cpu_baseline_legs(args, n):
     """cpu_baseline (1 thread, the reference is serial) and the same path
-    batch-parallel over this box's CPU share."""
+    batch-parallel over the threads host_threads() names:
+    the field says how many threads ran and why, next to the CPUs visible."""
     out = {}
     if args.config == 1 and args.op == "fwd":
         # config 1: the serial single forward of main.cu, for p-I and the
@@ -340,8 +372,11 @@ def cpu_baseline_legs(args, n):
         out[f"cpu_baseline_{other}"] = cpu_baseline("fwd", other, args.cpu_seconds / 2, 1)
         return out
     out["cpu_baseline"] = cpu_baseline(args.op, args.param, args.cpu_seconds, 1, args.ring)
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-    out["cpu_baseline_all_cores"] = cpu_baseline(args.op, args.param, args.cpu_seconds / 2, threads, args.ring)
+    threads, visible, why = host_threads()
+    par = cpu_baseline(args.op, args.param, args.cpu_seconds / 2, threads, args.ring)
+    par["cores_visible"] = visible
+    par["threads_reason"] = why
+    out["cpu_baseline_parallel"] = par
     if args.op == "nussbaumer":
         # the reference's own Nussbaumer shape: test_nussbaumer, n=1024 mod 2^32-1 (NTT.cu:1987-2005)
         out["cpu_baseline_reference_shape"] = cpu_baseline("nussbaumer", "p-I", args.cpu_seconds / 2, 1, "m32")

@@ -13,10 +13,15 @@
 #include "dev_tables.hpp"
 #include "ntt_device.hpp"
 #include "ntt_large.hpp"
+#include "ntt_wg.hpp"
 #include "ntt_internal.h"
 #include "params.hpp"
 #include "pset.hpp"
 
+#ifndef NTT_WGP
+#define NTT_WGP 0   // n = 2048 poly_ntt / poly_invntt on the workgroup-per-polynomial kernels (ntt_wg.hpp):
+                    // 1 persistent, 2 one polynomial per workgroup, 0 off
+#endif
 #ifndef QNTT_SRC_HASH
 #define QNTT_SRC_HASH "unknown"   // set by the Makefile: sha256 of the library sources
 #endif
@@ -54,6 +59,7 @@ struct DevInfo {
     bool tables = false;
     bool geo = false;
     int cus = 256;
+    int wgp_occ = 4;   // resident k_wg_xform workgroups per CU (occupancy API)
 };
 std::mutex g_dev_mutex;
 DevInfo g_dev[kMaxDev];
@@ -71,6 +77,10 @@ int device_ready(DevInfo **out)
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return hip_err(e);
         d.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_wg_xform<2, false, (NTT_WGP == 1)>, WGP_T, 0) == hipSuccess &&
+            occ > 0)
+            d.wgp_occ = occ;
         d.geo = true;
     }
     if (!d.tables) {
@@ -161,6 +171,20 @@ template <int PS> struct LXform {
             if (k == FWD) hipLaunchKernelGGL(k_ntt_fwd_large<PS>, g, b, 0, s, in, out, (uint32_t)batch, (uint32_t)ppw);
             else hipLaunchKernelGGL(k_ntt_inv_large<PS>, g, b, 0, s, in, out, (uint32_t)batch, (uint32_t)ppw);
         } else {
+#if NTT_WGP
+            if constexpr (PSel<PS>::T::N == 2048) {
+                // n = 2048 natural-order transforms: one polynomial per
+                // persistent 512-thread workgroup (ntt_wg.hpp)
+                if (k == FWD || k == INV) {
+                    constexpr bool PERSIST = NTT_WGP == 1;
+                    const size_t res = PERSIST ? (size_t)d.cus * d.wgp_occ : batch;
+                    const dim3 g((uint32_t)(batch < res ? batch : res)), b(WGP_T);
+                    if (k == FWD) hipLaunchKernelGGL((k_wg_xform<PS, false, PERSIST>), g, b, 0, s, in, out, (uint32_t)batch);
+                    else hipLaunchKernelGGL((k_wg_xform<PS, true, PERSIST>), g, b, 0, s, in, out, (uint32_t)batch);
+                    return finish_launch();
+                }
+            }
+#endif
             const Launch l = launch_for(OP_XFORM, PS, batch, d);
             const dim3 g(l.grid), b(NTT_WG);
             const uint32_t nb = (uint32_t)batch;

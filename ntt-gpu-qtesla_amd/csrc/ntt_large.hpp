@@ -60,7 +60,7 @@ struct Large {
     static constexpr int SLOTS = WAVES / G;   // polynomials per workgroup step
     static constexpr int NT = WAVES * 64;
     static constexpr int IDX = PS - LARGE_PS0;
-    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + G * TW2_WORDS + SLOTS;   // + slot counters
+    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + G * TW2_WORDS + SLOTS + 1;   // + slot counters, poison word
 };
 
 // global-order offset of sub-block B's outputs: brv_g(B)
@@ -76,14 +76,31 @@ __host__ __device__ constexpr uint32_t brv_g(uint32_t b, int logg) { return logg
 // (profiles/r02/s4/large/ab_slotsync_*.log).  The wait is bounded (2^22
 // short sleeps, ~0.1 s, far beyond any legitimate wait on partners resident
 // on the same CU) so that a broken schedule could never hang the GPU.
+//
+// An expired wait must not pass silently (the wave would go on with a
+// partner's buffer that is not written yet): it sets the workgroup's sticky
+// LDS poison word before the wave touches any buffer again, and every wave
+// re-reads that word after its last exchange read of a step and before the
+// step's stores -- a poisoned workgroup writes the non-canonical sentinel
+// 0xFFFFFFFF (>= q) for every remaining coefficient, so any range check on
+// the output sees it without a device sync.  A wave whose read saw a
+// partner's data of a later step reads the poison word after it, and LDS
+// requests of one wave are served in order, so it sees the poison too.  The
+// expiry is also counted on the device (ntt_sync_expiries; bench.py fails a
+// run whose count is not 0).
 #ifndef LARGE_SLOT_SYNC
 #define LARGE_SLOT_SYNC 1
 #endif
+#ifndef LARGE_SLOT_SYNC_SPIN
+#define LARGE_SLOT_SYNC_SPIN (1u << 22)   // 0 in the test build lib/libqtesla_ntt_syncfail.so: every wait expires
+#endif
+constexpr uint32_t SYNC_SENTINEL = 0xFFFFFFFFu;
 // count of slot-barrier waits that hit the bound (ntt_sync_expiries): 0 unless
-// the schedule broke; a launch that adds to it produced invalid results
+// the schedule broke; a launch that adds to it wrote sentinels
 __device__ unsigned int g_slot_sync_expired;
 struct SlotSync {
     uint32_t *ctr;
+    uint32_t *poison;   // the workgroup's sticky poison word
     uint32_t target;
     template <int G>
     __device__ __forceinline__ void wait()
@@ -93,18 +110,28 @@ struct SlotSync {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         bool arrived = false;
-        for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
+        for (uint32_t spin = 0; spin < (uint32_t)LARGE_SLOT_SYNC_SPIN; ++spin) {
             if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
                 arrived = true;
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        if (!arrived && (threadIdx.x & 63) == 0) atomicAdd(&g_slot_sync_expired, 1u);
+        if (!__builtin_amdgcn_readfirstlane((uint32_t)arrived)) {
+            if ((threadIdx.x & 63) == 0) {
+                __hip_atomic_store(poison, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                atomicAdd(&g_slot_sync_expired, 1u);
+            }
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #else
         __syncthreads();
 #endif
+    }
+    // after the step's last exchange read: store sentinels from here on?
+    __device__ __forceinline__ bool poisoned() const
+    {
+        return __builtin_amdgcn_readfirstlane(__hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0u;
     }
 };
 
@@ -199,9 +226,9 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
     const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + B * TW2_WORDS);
     fill_large_tw<LG, false>(lds);
     uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + G * TW2_WORDS;
-    if (threadIdx.x < (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;
+    if (threadIdx.x <= (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;   // slot counters + poison word
     __syncthreads();
-    SlotSync ss{ctrs + slot, 0};
+    SlotSync ss{ctrs + slot, ctrs + LG::SLOTS, 0};
     const LT L;
     const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
 #pragma unroll 1
@@ -238,9 +265,10 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
         }
         ss.wait<G>();   // the buffers are free for the next step's exchanges
         if (valid) {
+            const bool bad = ss.poisoned();
             uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
 #pragma unroll
-            for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, r[j]);
+            for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, bad ? SYNC_SENTINEL : r[j]);
         }
     }
 }
@@ -263,9 +291,9 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
     const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + B * TW2_WORDS);
     fill_large_tw<LG, true>(lds);
     uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + G * TW2_WORDS;
-    if (threadIdx.x < (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;
+    if (threadIdx.x <= (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;   // slot counters + poison word
     __syncthreads();
-    SlotSync ss{ctrs + slot, 0};
+    SlotSync ss{ctrs + slot, ctrs + LG::SLOTS, 0};
     const LT L;
     const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
 #pragma unroll 1
@@ -300,9 +328,10 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
         constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1)
         cross_gs<P, G>(r, buf, lds + (wave ^ D0) * XPOSE_WORDS, L.lane, (B & D0) != 0, c_cross[LG::IDX][1][1], ss);
         if (valid) {
+            const bool bad = ss.poisoned();
             uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
 #pragma unroll
-            for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, csub<P::Q>(r[j]));
+            for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, bad ? SYNC_SENTINEL : csub<P::Q>(r[j]));
         }
     }
 }

@@ -133,7 +133,7 @@ extern "C" int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uin
                                  void *stream)
 {
     const ParamSet *p = param_set(ps);
-    if (!p) return NTT_ERR_PARAM;
+    if (!p || ps > 2) return NTT_ERR_PARAM;   // the n = 4096 / 8192 sets have no variants here
     if (batch == 0) return NTT_OK;
     if (!d_in || !d_out) return NTT_ERR_NULL;
     if ((((uintptr_t)d_in) | ((uintptr_t)d_out)) & 15u) return NTT_ERR_ALIGN;
@@ -163,6 +163,7 @@ extern "C" int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uin
     switch (ps) {
     case 0: return launch<0>(op, variant, d_out, d_in, (uint32_t)batch, s);
     case 1: return launch<1>(op, variant, d_out, d_in, (uint32_t)batch, s);
-    default: return launch<2>(op, variant, d_out, d_in, (uint32_t)batch, s);
+    case 2: return launch<2>(op, variant, d_out, d_in, (uint32_t)batch, s);
+    default: return NTT_ERR_PARAM;
     }
 }

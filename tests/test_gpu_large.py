@@ -152,3 +152,36 @@ def test_large_slot_barriers_never_expire(ntt, oracle, dev, ps):
         assert torch.equal(x, ref)
     torch.cuda.synchronize()
     assert ntt.sync_expiries() == 0
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+def test_large_expired_slot_barrier_writes_sentinel(ntt, dev, ps):
+    """An expired slot-barrier wait fails loudly: in the test build whose
+    waits always expire (lib/libqtesla_ntt_syncfail.so, LARGE_SLOT_SYNC_SPIN=0,
+    the same sources), every stored coefficient is the non-canonical sentinel
+    0xFFFFFFFF (>= q, caught by any range check without a device sync) and
+    the device counter behind ntt_sync_expiries() counts the expiries."""
+    import ctypes
+    import os
+    path = os.path.join(os.path.dirname(ntt.LIB_PATH), "libqtesla_ntt_syncfail.so")
+    if not os.path.exists(path):
+        pytest.fail(f"{path} missing: build with `make -C ntt-gpu-qtesla_amd`")
+    ntt.lib()   # the HIP runtime torch loaded is bound first
+    L = ctypes.CDLL(path)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.poly_ntt.argtypes = [vp, vp, sz, ctypes.c_int, vp]
+    L.poly_invntt.argtypes = [vp, vp, sz, ctypes.c_int, vp]
+    L.ntt_sync_expiries.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
+    psn = ntt.PARAM_SETS[ps]
+    n = ntt.param_info(ps)["n"]
+    for fn in (L.poly_ntt, L.poly_invntt):
+        x = torch.empty(37 * n, dtype=torch.int32, device=dev)
+        ntt.fill_uniform(x, ps, 0x5E17, 0)
+        torch.cuda.synchronize()
+        assert fn(x.data_ptr(), None, 37, psn, None) == 0
+        torch.cuda.synchronize()
+        assert bool((x == -1).all()), "expired waits must write the sentinel everywhere"
+    c = ctypes.c_uint32(0)
+    assert L.ntt_sync_expiries(ctypes.byref(c)) == 0
+    assert c.value > 0
+    assert ntt.sync_expiries() == 0   # the product library's own counter is untouched
