@@ -741,6 +741,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_bitrev(const uin
     chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
 }
 
+
 // fused c = a*b mod (x^n+1): FWD(a), FWD(b) down to residues mod x^8 -+ zeta,
 // their products (BaseMul; the 2^-32 of its REDC and the (n/8)^-1 are folded
 // into the inverse's final scaling), INV from those residues -- one HBM read
@@ -750,7 +751,10 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_bitrev(const uin
 // completely and multiplied pointwise (Montgomery) -- two transforms of work
 // per product instead of three (poly_mul_ntt).  a, b and c may alias (no
 // __restrict__): every lane loads its words before it stores any.
-template <int PS, bool BHAT>
+// VAR (tools/ntt_diag.hip only, bottleneck attribution): 1 = global loads
+// and stores only (no arithmetic, no LDS), 2 = arithmetic + LDS only
+// (register-made inputs, outputs kept live, nothing stored).
+template <int PS, bool BHAT, int VAR = 0>
 __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
 {
     using P = typename PSel<PS>::T;
@@ -782,16 +786,35 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
         // a first, then b: the transpose's memory fences keep b's loads below
         // a's transform, so only ~64 coefficients are live at the peak
         uint32_t ra[32], rb[32];
-        load32(ra, a + ubase + loff, [](int j) { return LT::S * j; });
+        if constexpr (VAR == 2) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) ra[j] = (u + (uint32_t)j * 0x01000193u + L.lane) & 0x1FFFFFFFu;   // < q
+        } else {
+            load32(ra, a + ubase + loff, [](int j) { return LT::S * j; });
+        }
+        if constexpr (VAR == 1) {
+            load32(rb, b + ubase + loff, [](int j) { return LT::S * j; });
+            uint32_t *pc = c + ubase + off;
+#pragma unroll
+            for (int j = 0; j < 32; ++j)
+                if (valid) st_out(pc + LT::S * j, ra[j] + rb[j]);
+            continue;
+        }
         fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
         lds_p1_to_p2<P>(ra, buf, BHAT ? L : LT(opaque_lane()));
         fwd_pass2<P, BHAT ? 0 : mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
         // b-hat is in natural order: register j of the pass-2 layout holds
         // index brv5(j)*S + lane (the forward's store mapping)
-        load32(rb, b + ubase + loff, [](int j) { return LT::S * (BHAT ? brv5(j) : (uint32_t)j); });
+        if constexpr (VAR == 2) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) rb[j] = (u + (uint32_t)j * 0x00FF0101u + L.lane) & 0x1FFFFFFFu;
+        } else {
+            load32(rb, b + ubase + loff, [](int j) { return LT::S * (BHAT ? brv5(j) : (uint32_t)j); });
+        }
         uint32_t *pc = c + ubase + off;
         auto emit = [&](int j, uint32_t v) {   // stores interleaved with the last stage (see inv_pass1)
-            if (valid) st_out(pc + LT::S * j, v);
+            if constexpr (VAR == 2) asm volatile("" ::"v"(v));
+            else if (valid) st_out(pc + LT::S * j, v);
         };
         if constexpr (!BHAT) {
             // incomplete domain: both forwards stop above pos bit LOGR-1,

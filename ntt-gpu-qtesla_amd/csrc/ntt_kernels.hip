@@ -13,15 +13,17 @@
 #include "dev_tables.hpp"
 #include "ntt_device.hpp"
 #include "ntt_large.hpp"
-#include "ntt_wg.hpp"
-#include "ntt_internal.h"
-#include "params.hpp"
-#include "pset.hpp"
-
 #ifndef NTT_WGP
 #define NTT_WGP 0   // n = 2048 poly_ntt / poly_invntt on the workgroup-per-polynomial kernels (ntt_wg.hpp):
                     // 1 persistent, 2 one polynomial per workgroup, 0 off
 #endif
+#if NTT_WGP
+#include "ntt_wg.hpp"   // measured slower; A/B builds only
+#endif
+#include "ntt_internal.h"
+#include "params.hpp"
+#include "pset.hpp"
+
 #ifndef QNTT_SRC_HASH
 #define QNTT_SRC_HASH "unknown"   // set by the Makefile: sha256 of the library sources
 #endif
@@ -77,10 +79,12 @@ int device_ready(DevInfo **out)
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return hip_err(e);
         d.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+#if NTT_WGP
         int occ = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_wg_xform<2, false, (NTT_WGP == 1)>, WGP_T, 0) == hipSuccess &&
             occ > 0)
             d.wgp_occ = occ;
+#endif
         d.geo = true;
     }
     if (!d.tables) {

@@ -9,6 +9,8 @@
 //   variant 3  load + LDS transpose(s) + store (no arithmetic)
 //   op 2       plain copies of n=2048 polys, one per wave: dword (variant 0)
 //              or dwordx4 (variant 1) accesses
+//   op 3       k_poly_mul (d_out = in * in): variant 0 full, 1 global loads +
+//              stores only, 2 arithmetic + LDS only (k_poly_mul's VAR)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -115,6 +117,19 @@ int launch(int op, int variant, uint32_t *out, const uint32_t *in, uint32_t nb, 
     case 2: QNTT_V(false, 2); break;
     case 3: QNTT_V(false, 3); break;
     case 16: hipLaunchKernelGGL((k_ntt_inv<PS, false>), g, b, 0, s, in, out, nb, ppw); break;
+    case 48:
+    case 49:
+    case 50: {
+        // the library's poly_mul launch shape (launch_for(OP_MUL)): 4 workgroups per CU
+        constexpr int W = mul_wg<PS>() / 64;
+        uint32_t mp = units / (W * 4 * g_cus);
+        mp = mp < 1 ? 1 : (mp > 16 ? 16 : mp);
+        const dim3 gm((units + W * mp - 1) / (W * mp)), bm(mul_wg<PS>());
+        if (variant == 0) hipLaunchKernelGGL((k_poly_mul<PS, false, 0>), gm, bm, 0, s, in, in, out, nb, mp);
+        else if (variant == 1) hipLaunchKernelGGL((k_poly_mul<PS, false, 1>), gm, bm, 0, s, in, in, out, nb, mp);
+        else hipLaunchKernelGGL((k_poly_mul<PS, false, 2>), gm, bm, 0, s, in, in, out, nb, mp);
+        break;
+    }
     case 17: QNTT_V(true, 1); break;
     case 18: QNTT_V(true, 2); break;
     case 19: QNTT_V(true, 3); break;
@@ -159,7 +174,7 @@ extern "C" int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uin
         else hipLaunchKernelGGL((k_copy_diag<4>), g2, dim3(512), 0, s, d_in, d_out, (uint32_t)batch);
         return hipGetLastError() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
     }
-    if (op != 0 && op != 1) return NTT_ERR_PARAM;
+    if (op != 0 && op != 1 && op != 3) return NTT_ERR_PARAM;
     switch (ps) {
     case 0: return launch<0>(op, variant, d_out, d_in, (uint32_t)batch, s);
     case 1: return launch<1>(op, variant, d_out, d_in, (uint32_t)batch, s);

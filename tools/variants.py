@@ -42,6 +42,8 @@ def main():
             names[f"{opn}_{vn}"] = (op, v)
     names["copy_dword"] = (2, 0)
     names["copy_x4"] = (2, 1)
+    for v, vn in ((0, "full"), (1, "mem"), (2, "alu")):
+        names[f"mul_{vn}"] = (3, v)   # k_poly_mul<PS,false,VAR>: c = x * x
     todo = list(names) + ["torch_copy"]
     if args.only:
         todo = [t for t in todo if t in args.only.split(",")]
@@ -66,12 +68,13 @@ def main():
             e1.record(s)
             e1.synchronize()
             res[t].append(e0.elapsed_time(e1))
-    bytes_ = args.batch * n * 8
     out = {}
     for t, v in res.items():
         v.sort()
         med = v[len(v) // 2]
+        bytes_ = args.batch * n * (12 if t.startswith("mul_") else 8)
         out[t] = {"ms_median": med, "ms_min": v[0], "GBps_alg": bytes_ / (med * 1e-3) / 1e9}
+    bytes_ = args.batch * n * 8
     print(json.dumps({"param": args.param, "batch": args.batch, "bytes_per_launch": bytes_, "results": out}, indent=1))
 
 
