@@ -265,16 +265,28 @@ def main():
             launch(k)
     torch.cuda.synchronize(device)
 
+    # Kernel durations from HIP events on the launch stream.  With several
+    # kinds per step (fwd + inv) every launch has its own event pair; with one
+    # kind the pair brackets the whole timed region and the average is
+    # region / steps: per-launch event pairs add ~5 us to a ~0.1 ms launch
+    # (config 2: 117.8 us per-launch events vs rocprofv3 111.8 us).
+    single = len(kinds) == 1
     evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in kinds]
-           for _ in range(args.steps)]
+           for _ in range(1 if single else args.steps)]
     dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
+    if single:
+        evs[0][0][0].record(stream)
     for s in range(args.steps):
         for i, k in enumerate(kinds):
-            evs[s][i][0].record(stream)
+            if not single:
+                evs[s][i][0].record(stream)
             launch(k)
-            evs[s][i][1].record(stream)
+            if not single:
+                evs[s][i][1].record(stream)
+    if single:
+        evs[0][0][1].record(stream)
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
     dist.barrier()
@@ -287,8 +299,11 @@ def main():
         torch.cuda.synchronize(device)
         expiries = ntt_amd.sync_expiries()
 
-    per_kind = {k: sum(evs[s][i][0].elapsed_time(evs[s][i][1]) for s in range(args.steps)) / args.steps
-                for i, k in enumerate(kinds)}  # ms per launch
+    if single:
+        per_kind = {kinds[0]: evs[0][0][0].elapsed_time(evs[0][0][1]) / args.steps}
+    else:
+        per_kind = {k: sum(evs[s][i][0].elapsed_time(evs[s][i][1]) for s in range(args.steps)) / args.steps
+                    for i, k in enumerate(kinds)}  # ms per launch
     dom = max(per_kind, key=per_kind.get)
     bytes_per_coeff = 12 if dom in ("mul", "mulntt", "nus") else 8
     alg_bytes = count * n * bytes_per_coeff
@@ -334,6 +349,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                      "avg_launch_ms": per_kind[dom], "alg_bytes_per_launch": alg_bytes,
+                     "timing": "region events / steps" if single else "per-launch events",
                      "per_kernel_ms": per_kind},
         "check": check,
         "build": {"hash": build_hash},

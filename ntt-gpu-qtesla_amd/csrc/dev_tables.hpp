@@ -94,6 +94,37 @@ inline hipError_t upload_large_tables(int ps, const Tables &t)
                 return e;
         }
         for (uint32_t k = 1; k < G; k++) dev_pair(p, t, inv != 0, k, cross[k].x, cross[k].y);
+        // sub-tree scale factors (c_fscale, ntt_large.hpp): c_{B,b} = T_B[k'] / T_0[k']
+        // at k' = 2^(10-b) (the same ratio for every k' of stage b), and
+        // F_B[j] = prod over the set bits b of j of c_{B,b}, as Shoup pairs
+        {
+            const std::vector<uint32_t> &tw = inv ? t.inv : t.fwd;
+            auto mulq = [&](uint64_t a, uint64_t b) { return (uint32_t)(a * b % p.q); };
+            auto powq = [&](uint64_t a, uint64_t e) {
+                uint64_t r = 1;
+                for (a %= p.q; e; e >>= 1, a = a * a % p.q)
+                    if (e & 1) r = r * a % p.q;
+                return (uint32_t)r;
+            };
+            uint2 fs[LARGE_GMAX][32] = {};
+            for (uint32_t B = 0; B < G; B++) {
+                uint32_t c[5];
+                for (int b = 0; b < 5; b++) {
+                    const uint32_t kp = 1u << (10 - b);
+                    c[b] = mulq(tw[2 * sub_tree_k(kp, G, B)], powq(tw[2 * sub_tree_k(kp, G, 0)], p.q - 2));
+                }
+                for (uint32_t j = 0; j < 32; j++) {
+                    uint32_t f = 1;
+                    for (int b = 0; b < 5; b++)
+                        if ((j >> b) & 1) f = mulq(f, c[b]);
+                    fs[B][j].x = f;
+                    fs[B][j].y = cshoup(f, p.q);
+                }
+            }
+            if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_fscale), fs, sizeof fs, (size_t)(idx * 2 + inv) * sizeof fs,
+                                       hipMemcpyHostToDevice)) != hipSuccess)
+                return e;
+        }
         if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_subtw), sub, sizeof sub, (size_t)(idx * 2 + inv) * sizeof sub,
                                    hipMemcpyHostToDevice)) != hipSuccess)
             return e;

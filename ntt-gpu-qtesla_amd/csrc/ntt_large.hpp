@@ -43,8 +43,24 @@ __constant__ uint2 c_subtw[LARGE_NPS][2][LARGE_GMAX][32];
 __constant__ uint2 c_cross[LARGE_NPS][2][4];
 // last sub-tree inverse stage: n^-1 psi^-brv(2^g + B), centred signed pair
 __constant__ uint2 c_lastinv[LARGE_NPS][LARGE_GMAX];
-// LDS images (lane twiddles + bit-5 table) of T_B, [set][fwd/inv][B]
+// LDS images (lane twiddles + bit-5 table) of T_B, [set][fwd/inv][B]; the
+// kernels copy the lane twiddles of B = 0 only (shared, see c_fscale) and the
+// 32-entry bit-5 table of every B
 __device__ uint4 g_tw2imgL[LARGE_NPS][2][LARGE_GMAX][TW2_VEC4];
+// Sub-tree twiddles share one table: for every stage b of the 2048-point
+// sub-transform T_B[k'] = c_{B,b} T_0[k'] (one constant per (B, b);
+// tests/test_oracle_large.py checks it for both sets and directions).  So the
+// pass-2 stages (bits 4..0 of the sub-block position) run on T_0's lane
+// table for every B once the forward has multiplied register j of the
+// pass-2 layout (position 32 Lp + j) by F_B[j] = prod_{bit b of j} c_{B,b}
+// (that factor is common to both inputs of every butterfly of the earlier
+// stages, so it may enter anywhere before pass 2, and each pass-2 stage b
+// then consumes exactly its c_{B,b}); the inverse multiplies by
+// G_B[j] = prod_{bit b of j} c'_{B,b} after its pass-2 GS stages, which leave
+// every value short of exactly that factor.  Shoup pairs (F, F'),
+// [set][fwd/inv][B][j]; B = 0 is all ones and skipped.  Three of the four
+// 15.75 KiB LDS images (n = 8192) are freed: 16 waves per workgroup instead of 12.
+__constant__ uint2 c_fscale[LARGE_NPS][2][LARGE_GMAX][32];
 
 template <int PS>
 struct Large {
@@ -53,14 +69,21 @@ struct Large {
     static_assert(PL::Q == P::Q, "large-n sets use p-III's prime");
     static constexpr int G = (int)(PL::N / 2048);
     static constexpr int LOGG = G == 2 ? 1 : 2;
-    // 16 waves x 8 KiB + 2 x 15.75 KiB tables / 12 waves x 8 KiB + 4 x 15.75
-    // KiB: one workgroup per CU, 4 / 3 waves per SIMD
-    static constexpr int WAVES = G == 2 ? 16 : 12;
+    // One workgroup per CU at 4 waves per SIMD: 16 waves x 8 KiB + the
+    // twiddle tables.  n = 4096: both sub-tree tables (2 x 15.75 KiB);
+    // n = 8192: four would only leave room for 12 waves, so the sub-trees
+    // share T_0's lane table and scale by c_fscale (SHARED): 4.94 / 4.75 ->
+    // 4.62 / 4.59 ms fwd / inv per 2^18 polys, while at n = 4096 the scaling
+    // only costs (3.98 / 3.97 -> 4.20 / 4.04 ms), profiles/r03/ab_l*_tab.log
+    static constexpr int WAVES = 16;
+    static constexpr bool SHARED = G == 4;
     static constexpr int OCC = WAVES / 4;
     static constexpr int SLOTS = WAVES / G;   // polynomials per workgroup step
     static constexpr int NT = WAVES * 64;
     static constexpr int IDX = PS - LARGE_PS0;
-    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + G * TW2_WORDS + SLOTS + 1;   // + slot counters, poison word
+    // lane tables (shared: T_0's + per-B bit-5 tables; else G whole images)
+    static constexpr int TAB_WORDS = SHARED ? TW2_WORDS + G * 64 : G * TW2_WORDS;
+    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + TAB_WORDS + SLOTS + 1;   // + slot counters, poison word
 };
 
 // global-order offset of sub-block B's outputs: brv_g(B)
@@ -195,14 +218,34 @@ __device__ __forceinline__ uint32_t xch_pos(uint32_t kp, uint32_t B)
     return (kp + B * (32u / G)) & 2047u;
 }
 
-// The workgroup's G lane-twiddle images of one direction (contiguous in
-// g_tw2imgL) into LDS after the transpose buffers.
+// The workgroup's twiddle tables of one direction into LDS after the
+// transpose buffers: T_0's lane image, then the bit-5 table of every B.
+constexpr int TW2_BIT5_VEC4 = TW2_ENTRIES * 64 * 2 / 4;   // uint4 offset of the bit-5 table in an image
 template <class LG, bool INV>
 __device__ __forceinline__ void fill_large_tw(uint32_t *lds)
 {
-    const uint4 *src = g_tw2imgL[LG::IDX][INV ? 1 : 0][0];
     uint4 *dst = reinterpret_cast<uint4 *>(lds + LG::WAVES * XPOSE_WORDS);
-    for (int i = threadIdx.x; i < LG::G * TW2_VEC4; i += LG::NT) dst[i] = src[i];
+    if constexpr (!LG::SHARED) {   // the G images, contiguous in g_tw2imgL
+        const uint4 *src = g_tw2imgL[LG::IDX][INV ? 1 : 0][0];
+        for (int i = threadIdx.x; i < LG::G * TW2_VEC4; i += LG::NT) dst[i] = src[i];
+        return;
+    }
+    for (int i = threadIdx.x; i < TW2_BIT5_VEC4 + LG::G * 16; i += LG::NT) {
+        const int b = i < TW2_BIT5_VEC4 ? 0 : (i - TW2_BIT5_VEC4) >> 4;
+        const int o = i < TW2_BIT5_VEC4 ? i : TW2_BIT5_VEC4 + ((i - TW2_BIT5_VEC4) & 15);
+        dst[i] = g_tw2imgL[LG::IDX][INV ? 1 : 0][b][o];
+    }
+}
+
+// register j of the pass-2 layout times F_B[j] / G_B[j] (Shoup, output in [0, 2q))
+template <class P, class LG, bool INV>
+__device__ __forceinline__ void subtree_scale(uint32_t (&r)[32], uint32_t B)
+{
+    if constexpr (!LG::SHARED) return;
+    if (B == 0) return;   // wave-uniform
+    const uint2 *f = c_fscale[LG::IDX][INV ? 1 : 0][B] + opaque_zero();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) r[j] = shoup_mul<P::Q>(r[j], f[j].x, f[j].y);
 }
 
 // Workgroup b owns polynomials [b SLOTS ppw, (b+1) SLOTS ppw); slot s of a
@@ -223,9 +266,12 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
     if (first >= npoly) return;   // whole workgroup
     const uint32_t wave = wave_id(), B = wave % G, slot = wave / G;
     uint32_t *const buf = lds + wave * XPOSE_WORDS;
-    const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + B * TW2_WORDS);
+    // lane table (T_0's when SHARED, else T_B's image) and T_B's bit-5 table
+    const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + (LG::SHARED ? 0u : B * TW2_WORDS));
+    const uint2 *bit5 = LG::SHARED ? reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + TW2_BIT5_VEC4 * 4 + B * 64)
+                                   : tw2 + TW2_ENTRIES * 64;
     fill_large_tw<LG, false>(lds);
-    uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + G * TW2_WORDS;
+    uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + LG::TAB_WORDS;
     if (threadIdx.x <= (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;   // slot counters + poison word
     __syncthreads();
     SlotSync ss{ctrs + slot, ctrs + LG::SLOTS, 0};
@@ -247,8 +293,9 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
         if constexpr (G == 4)
             cross_ct<P, true, G>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0,
                                  c_cross[LG::IDX][0][2 + (B >> 1)], ss);
-        fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), tw2 + TW2_ENTRIES * 64 + opaque_zero());
-        lds_p1_to_p2<P>(r, buf, L);
+        fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), bit5 + opaque_zero());
+        lds_p1_to_p2<P>(r, buf, LT(opaque_lane()));   // addresses recomputed (see k_ntt_inv_large)
+        subtree_scale<P, LG, false>(r, B);             // T_B = c_{B,b} T_0 (c_fscale)
         fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
         // all-to-all through the exchange buffers: register j of lane l holds
         // k' = brv5(j) 64 + l, global index G k' + brv_g(B); this wave then
@@ -288,9 +335,12 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
     if (first >= npoly) return;
     const uint32_t wave = wave_id(), B = wave % G, slot = wave / G;
     uint32_t *const buf = lds + wave * XPOSE_WORDS;
-    const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + B * TW2_WORDS);
+    // lane table (T_0's when SHARED, else T_B's image) and T_B's bit-5 table
+    const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + (LG::SHARED ? 0u : B * TW2_WORDS));
+    const uint2 *bit5 = LG::SHARED ? reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + TW2_BIT5_VEC4 * 4 + B * 64)
+                                   : tw2 + TW2_ENTRIES * 64;
     fill_large_tw<LG, true>(lds);
-    uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + G * TW2_WORDS;
+    uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + LG::TAB_WORDS;
     if (threadIdx.x <= (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;   // slot counters + poison word
     __syncthreads();
     SlotSync ss{ctrs + slot, ctrs + LG::SLOTS, 0};
@@ -319,8 +369,11 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
 #pragma unroll
         for (int j = 0; j < 32; ++j) r[j] = buf[xch_pos<G>(brv5(j) * 64 + L.lane, B)];
         inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
-        lds_p2_to_p1<P>(r, buf, L);
-        inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        subtree_scale<P, LG, true>(r, B);   // the c'_{B,b} the shared table left out (c_fscale)
+        // transpose addresses from an opaque lane: recomputed here instead of
+        // 8 loop-invariant VGPRs (which spilled at the 128-VGPR budget)
+        lds_p2_to_p1<P>(r, buf, LT(opaque_lane()));
+        inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5 + opaque_zero());
         const uint2 last = c_lastinv[LG::IDX][B];
         inv_last_stage<P, false>(r, LG::PL::NINV, NINVP, last.x, last.y);   // [0,2q), scaled by n^-1
         if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)

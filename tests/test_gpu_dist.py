@@ -51,3 +51,29 @@ def test_bench_two_ranks_counts_both(ntt):
     assert d["check"]["all_ranks_ok"] is True
     # value = polys of BOTH ranks / the max-over-ranks wall time
     assert abs(d["value"] - 2 * batch * steps / (d["ms_per_step"] * steps * 1e-3)) <= 1e-6 * d["value"]
+
+
+def test_bench_default_backend_is_gloo(ntt):
+    """The bench's only collectives are a barrier and a scalar max/min on
+    CPU tensors (north_star: no data-path collective), so the default
+    process group is gloo; the line names it and the per-rank spread."""
+    r = _torchrun([os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "4096", "--steps", "2",
+                   "--warmup", "1", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["config"]["dist_backend"] == "gloo"
+    spread = d["rank_ms_per_step"]
+    assert 0 < spread["min"] <= spread["max"] == pytest.approx(d["ms_per_step"])
+
+
+def test_bench_two_ranks_rccl(ntt):
+    """The RCCL (nccl) process group, kept as an option: exercised only where
+    two devices exist (RCCL refuses two ranks on one device)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("RCCL needs one device per rank; this box has one GPU")
+    r = _torchrun([os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "4096", "--steps", "2",
+                   "--warmup", "1", "--dist-backend", "nccl", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["config"]["dist_backend"] == "nccl" and d["check"]["all_ranks_ok"] is True

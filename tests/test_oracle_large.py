@@ -51,3 +51,30 @@ def test_large_polymul_schoolbook(oracle):
     a = oracle.fill_uniform(1, ps, 5, 0)
     b = oracle.fill_uniform(1, ps, 6, 0)
     assert np.array_equal(oracle.poly_mul(a, b, ps)[0], oracle.schoolbook_np(a[0], b[0], ps))
+
+
+@pytest.mark.parametrize("n", [4096, 8192])
+@pytest.mark.parametrize("direction", ["fwd", "inv"])
+def test_subtree_twiddles_factor(n, direction):
+    """ntt_large.hpp's shared sub-tree table: for sub-block B of the n-point
+    transform and every stage b of its 2048-point sub-transform, the twiddle
+    psi^(+-brv_L(2^(10-b) (G + B) + m)) equals c_{B,b} times sub-block 0's,
+    with one constant per (B, b) for all m (the kernels scale by products of
+    these constants instead of holding G lane tables)."""
+    q = 856145921
+    L = n.bit_length() - 1
+    G = n // 2048
+    psi = pow(3, (q - 1) // (2 * n), q)
+    root = psi if direction == "fwd" else pow(psi, q - 2, q)
+
+    def brv(k, bits):
+        return int(format(k, f"0{bits}b")[::-1], 2)
+
+    for B in range(G):
+        for b in range(11):
+            ratios = set()
+            for m in range(0, 1 << (10 - b), max(1, (1 << (10 - b)) // 64)):
+                kB = (1 << (10 - b)) * (G + B) + m
+                k0 = (1 << (10 - b)) * G + m
+                ratios.add(pow(root, brv(kB, L), q) * pow(pow(root, brv(k0, L), q), q - 2, q) % q)
+            assert len(ratios) == 1, (B, b)
