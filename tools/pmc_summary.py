@@ -37,7 +37,7 @@ def kernel_patterns(op, ps, ring):
                 "fwd": {"fwd": f"k_ntt_fwd_large<{ps}>"}, "inv": {"inv": f"k_ntt_inv_large<{ps}>"}}[op]
     return {"fwdinv": {"fwd": f"k_ntt_fwd<{ps}, false>", "inv": f"k_ntt_inv<{ps}, false>"},
             "fwd": {"fwd": f"k_ntt_fwd<{ps}, false>"}, "inv": {"inv": f"k_ntt_inv<{ps}, false>"},
-            "polymul": {"mul": f"k_poly_mul<{ps}, false>"}, "polymul_ntt": {"mulntt": f"k_poly_mul<{ps}, true>"},
+            "polymul": {"mul": f"k_poly_mul<{ps}, false, 0>"}, "polymul_ntt": {"mulntt": f"k_poly_mul<{ps}, true, 0>"},
             "nussbaumer": {"nus": f"k_nussbaumer<{ps if not (ring == 'm32' and ps == 0) else 1}, "
                                   f"{1 if ring == 'm32' else 0}>"}}[op]
 
