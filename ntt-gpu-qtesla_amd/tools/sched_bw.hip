@@ -171,6 +171,39 @@ __global__ __launch_bounds__(512) void k_deq(uint32_t *buf, uint32_t nunits, uin
     if (nunits == 0) dyn[threadIdx.x] = 0;
 }
 
+
+// ---- sync-stride: persistent grid-stride with bounded drift ----------------
+// step i of workgroup b is unit i * G8 + 8 b + w (one contiguous window of the
+// whole grid per step); after a step lane 0 of wave 0 adds 1 to the global
+// count of finished workgroup-steps, and before step i a workgroup waits
+// (bounded spin) until the grid has finished step i - K (count >= (i-K+1) G):
+// the window in flight then spans at most K+1 steps of the grid
+template <bool NT, int ITER, int K>
+__global__ __launch_bounds__(512) void k_sync_stride(uint32_t *buf, uint32_t nunits, uint32_t *done)
+{
+    extern __shared__ uint32_t dyn[];
+    const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t G = gridDim.x, G8 = G * 8;
+    for (uint32_t i = 0;; ++i) {
+        const uint32_t u = i * G8 + blockIdx.x * 8 + w;
+        if (i * G8 >= nunits) break;
+        if (i > K) {
+            if (threadIdx.x == 0) {
+                const uint32_t need = (i - K) * G;
+                for (uint32_t spin = 0; spin < (1u << 20); ++spin) {
+                    if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            __syncthreads();
+        }
+        if (u < nunits) unit_copy<NT, ITER>(buf, u, lane);
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (nunits == 0) dyn[threadIdx.x] = 0;
+}
+
 // ---- wgpoly: one polynomial per 512-thread workgroup ----------------------
 template <int ITER>
 __global__ __launch_bounds__(512) void k_wgpoly(uint32_t *buf, uint32_t nunits)
@@ -250,57 +283,40 @@ int main(int argc, char **argv)
         hipLaunchKernelGGL((k_burst<W, PER, WPB, NT, ITER>), dim3(grid), dim3(64 * WPB), LDS, 0, a, nwords);    \
     });
     // flat copies: access width and per-wave burst length
-    BURST(4, 1, 4, false, 0, 0)
-    BURST(1, 1, 4, false, 0, 0)
-    BURST(1, 4, 4, false, 0, 0)
-    BURST(4, 2, 4, false, 0, 0)
-    BURST(1, 8, 4, false, 0, 0)
-    BURST(1, 16, 4, false, 0, 0)
-    BURST(1, 32, 4, false, 0, 0)
-    BURST(1, 32, 8, false, 0, 0)
-    BURST(1, 32, 16, false, 0, 0)
-    BURST(1, 32, 8, true, 0, 0)
-    BURST(4, 8, 8, false, 0, 0)
-    BURST(4, 1, 4, false, 0, 40 * 1024)    // 4 WG x 4 waves = 16 waves/CU
-    BURST(1, 32, 8, false, 0, 80 * 1024)   // 16 waves/CU
-    BURST(1, 32, 8, true, 0, 80 * 1024)
-    BURST(1, 32, 8, true, 20, 0)
-    BURST(1, 32, 8, true, 40, 0)
-    BURST(1, 32, 8, true, 20, 80 * 1024)
-    BURST(1, 32, 8, true, 40, 80 * 1024)
 #define CHUNK(NT, ITER, PPW)                                                                                     \
     snprintf(nm, sizeof nm, "chunk nt=%d iter=%d ppw=%d lds=80K", NT, ITER, PPW);                               \
     add(nm, [=] {                                                                                                \
         const uint32_t grid = (npoly + 8 * PPW - 1) / (8 * PPW);                                                 \
         hipLaunchKernelGGL((k_chunk<NT, ITER>), dim3(grid), dim3(512), LDS80, 0, a, npoly, (uint32_t)PPW);     \
     });
-    CHUNK(true, 0, 16)
-    CHUNK(true, 0, 4)
-    CHUNK(true, 0, 1)
-    CHUNK(false, 0, 16)
-    CHUNK(true, 20, 16)
-    CHUNK(true, 40, 16)
 #define STRIDE(NT, ITER)                                                                                         \
     snprintf(nm, sizeof nm, "stride nt=%d iter=%d lds=80K", NT, ITER);                                          \
     add(nm, [=] { hipLaunchKernelGGL((k_stride<NT, ITER>), dim3(2 * cus), dim3(512), LDS80, 0, a, npoly); });
-    STRIDE(true, 0)
 #define DEQ(NT, ITER, G, WGPC)                                                                                   \
     snprintf(nm, sizeof nm, "deq nt=%d iter=%d group=%d wg/cu=%d", NT, ITER, G, WGPC);                          \
     add(nm, [=] {                                                                                                \
         CK(hipMemsetAsync(ctr, 0, 8 * 128, 0));                                                                  \
         hipLaunchKernelGGL((k_deq<NT, ITER, G>), dim3(WGPC * cus), dim3(512), (WGPC == 2 ? LDS80 : 40 * 1024), 0, a, npoly, ctr); \
     });
-    DEQ(true, 0, 8, 2)
-    DEQ(false, 0, 8, 2)
-    DEQ(true, 0, 64, 2)
-    DEQ(true, 0, 8, 4)
-    DEQ(true, 20, 8, 2)
-    DEQ(true, 40, 8, 2)
 #define WGPOLY(ITER)                                                                                             \
     snprintf(nm, sizeof nm, "wgpoly iter=%d", ITER);                                                             \
     add(nm, [=] { hipLaunchKernelGGL((k_wgpoly<ITER>), dim3(npoly), dim3(512), 0, 0, a, npoly); });
-    WGPOLY(0)
-    WGPOLY(20)
+
+#define SSTR(NT, ITER, K)                                                                                        \
+    snprintf(nm, sizeof nm, "sync-stride nt=%d iter=%d K=%d lds=80K", NT, ITER, K);                            \
+    add(nm, [=] {                                                                                                \
+        CK(hipMemsetAsync(ctr, 0, 8 * 128, 0));                                                                  \
+        hipLaunchKernelGGL((k_sync_stride<NT, ITER, K>), dim3(2 * cus), dim3(512), LDS80, 0, a, npoly, ctr);    \
+    });
+    SSTR(true, 0, 1)
+    SSTR(true, 0, 2)
+    SSTR(true, 0, 4)
+    SSTR(true, 0, 16)
+    CHUNK(true, 0, 16)
+    CHUNK(true, 0, 4)
+    STRIDE(true, 0)
+    BURST(4, 1, 4, false, 0, 0)
+    BURST(1, 32, 8, true, 0, 0)
     add("lib poly_ntt p-III", [=] {
         const int rc = poly_ntt(a, nullptr, npoly, NTT_PARAM_P_III, nullptr);
         if (rc) { fprintf(stderr, "poly_ntt rc=%d\n", rc); exit(3); }
