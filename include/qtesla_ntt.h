@@ -41,12 +41,11 @@ extern "C" {
 /* Larger transforms over p-III's prime (q - 1 = 2^14 * 52255 admits
  * negacyclic n up to 8192), for the reference's n > 2048 dataflows (its
  * Stockham / CT2 kernels, NTT.cu:1085-1153, 1268-1337, 667-951): multi-wave
- * four-step kernels.  For these sets:
- *   accepted: poly_ntt, poly_invntt, poly_ntt_oop, poly_invntt_oop,
- *             poly_pointwise, ntt_fill_uniform, ntt_param_info,
- *             ntt_get_tables, ntt_host_ctx_create and its *_host transforms;
- *   NTT_ERR_PARAM: poly_ntt_bitrev, poly_invntt_bitrev, poly_bitrev_copy,
- *             poly_mul, poly_mul_ntt, poly_mul_nussbaumer (and poly_mul_host). */
+ * four-step kernels.  For these sets every entry point is accepted except
+ * poly_mul_nussbaumer (NTT_ERR_PARAM: its split is defined for n = 1024 /
+ * 2048).  poly_mul / poly_mul_ntt are one fused launch; poly_bitrev_copy is
+ * one launch; poly_ntt_bitrev / poly_invntt_bitrev are two (the natural-order
+ * transform and the bit-reversal, in that / the opposite order). */
 #define NTT_PARAM_N4096 3 /* n = 4096, q = 856145921, psi = 3^((q-1)/2n)    */
 #define NTT_PARAM_N8192 4 /* n = 8192, q = 856145921, psi = 3^((q-1)/2n)    */
 

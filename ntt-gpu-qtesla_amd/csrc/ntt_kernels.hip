@@ -159,6 +159,14 @@ int dispatch(int ps, Args... args)
     }
 }
 
+// n = 4096 / 8192: polynomials per slot and step count, >= 2 workgroups per CU
+template <class LG>
+size_t large_ppw(size_t batch, const DevInfo &d)
+{
+    size_t ppw = batch / ((size_t)LG::SLOTS * d.cus * 2);
+    return ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
+}
+
 // transform kind: forward / inverse with natural or bit-reversed NTT-domain
 // order, or the plain bit-reversal permutation
 enum Xform { FWD, INV, FWD_BR, INV_BR, BITREV };
@@ -166,14 +174,27 @@ enum Xform { FWD, INV, FWD_BR, INV_BR, BITREV };
 template <int PS> struct LXform {
     static int run(Xform k, const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s, const DevInfo &d)
     {
-        if constexpr (PS >= LARGE_PS0) {   // n = 4096 / 8192: natural-order transforms only
+        if constexpr (PS >= LARGE_PS0) {
+            // n = 4096 / 8192: the natural-order transforms; the bit-reversed
+            // orders compose them with the bit-reversal kernel (2 launches)
             using LG = Large<PS>;
-            if (k != FWD && k != INV) return NTT_ERR_PARAM;
-            size_t ppw = batch / ((size_t)LG::SLOTS * d.cus * 2);
-            ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
+            const uint32_t nb = (uint32_t)batch;
+            const size_t ppw = large_ppw<LG>(batch, d);
             const dim3 g((uint32_t)((batch + LG::SLOTS * ppw - 1) / (LG::SLOTS * ppw))), b(LG::NT);
-            if (k == FWD) hipLaunchKernelGGL(k_ntt_fwd_large<PS>, g, b, 0, s, in, out, (uint32_t)batch, (uint32_t)ppw);
-            else hipLaunchKernelGGL(k_ntt_inv_large<PS>, g, b, 0, s, in, out, (uint32_t)batch, (uint32_t)ppw);
+            const dim3 gb((uint32_t)(batch < (size_t)d.cus * 64 ? batch : (size_t)d.cus * 64)), bb(512);
+            switch (k) {
+            case FWD: hipLaunchKernelGGL(k_ntt_fwd_large<PS>, g, b, 0, s, in, out, nb, (uint32_t)ppw); break;
+            case INV: hipLaunchKernelGGL(k_ntt_inv_large<PS>, g, b, 0, s, in, out, nb, (uint32_t)ppw); break;
+            case BITREV: hipLaunchKernelGGL(k_bitrev_large<PS>, gb, bb, 0, s, in, out, nb); break;
+            case FWD_BR:
+                hipLaunchKernelGGL(k_ntt_fwd_large<PS>, g, b, 0, s, in, out, nb, (uint32_t)ppw);
+                hipLaunchKernelGGL(k_bitrev_large<PS>, gb, bb, 0, s, out, out, nb);
+                break;
+            case INV_BR:
+                hipLaunchKernelGGL(k_bitrev_large<PS>, gb, bb, 0, s, in, out, nb);
+                hipLaunchKernelGGL(k_ntt_inv_large<PS>, g, b, 0, s, out, out, nb, (uint32_t)ppw);
+                break;
+            }
         } else {
 #if NTT_WGP
             if constexpr (PSel<PS>::T::N == 2048) {
@@ -203,12 +224,22 @@ template <int PS> struct LXform {
         return finish_launch();
     }
 };
+template <int PS, bool BHAT>
+void launch_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s, const DevInfo &d)
+{
+    using LG = Large<PS, mul_large_waves<PS, BHAT>()>;
+    const size_t ppw = large_ppw<LG>(batch, d);
+    const dim3 g((uint32_t)((batch + LG::SLOTS * ppw - 1) / (LG::SLOTS * ppw))), blk(LG::NT);
+    hipLaunchKernelGGL((k_poly_mul_large<PS, BHAT>), g, blk, 0, s, a, b, c, (uint32_t)batch, (uint32_t)ppw);
+}
 template <int PS> struct LMul {
     static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s, bool bhat,
                    const DevInfo &d)
     {
         if constexpr (PS >= LARGE_PS0) {
-            return NTT_ERR_PARAM;   // no fused product for n > 2048
+            if (bhat) launch_mul_large<PS, true>(a, b, c, batch, s, d);
+            else launch_mul_large<PS, false>(a, b, c, batch, s, d);
+            return finish_launch();
         } else {
             const Launch l = launch_for(OP_MUL, PS, batch, d);
             const dim3 g(l.grid), blk(mul_wg<PS>());
@@ -234,7 +265,6 @@ int transform(Xform k, uint32_t *out, const uint32_t *in, size_t batch, int ps, 
     if (rc == NTT_OK && batch) rc = check_common(ps, out, batch);
     if (rc != NTT_OK || batch == 0) return rc;
     if (partial_overlap(in, out, batch * param_set(ps)->n * 4)) return NTT_ERR_ALIAS;
-    if (param_set(ps)->n > 2048 && k != FWD && k != INV) return NTT_ERR_PARAM;   // natural order only
     DevInfo *d = nullptr;
     if ((rc = device_ready(&d)) != NTT_OK) return rc;
     return dispatch<LXform>(ps, k, in, out, batch, (hipStream_t)stream, *d);
@@ -249,7 +279,6 @@ int mul_common(uint32_t *d_c, const uint32_t *d_a, const uint32_t *d_b, size_t b
     if ((rc = check_common(ps, d_c, batch)) != NTT_OK) return rc;
     const size_t bytes = batch * param_set(ps)->n * 4;
     if (partial_overlap(d_a, d_c, bytes) || partial_overlap(d_b, d_c, bytes)) return NTT_ERR_ALIAS;
-    if (param_set(ps)->n > 2048) return NTT_ERR_PARAM;   // no fused product at n > 2048
     DevInfo *d = nullptr;
     if ((rc = device_ready(&d)) != NTT_OK) return rc;
     return dispatch<LMul>(ps, d_a, d_b, d_c, batch, (hipStream_t)stream, bhat, *d);

@@ -41,8 +41,9 @@ constexpr int LARGE_GMAX = 4;   // waves per polynomial at n = 8192
 __constant__ uint2 c_subtw[LARGE_NPS][2][LARGE_GMAX][32];
 // twiddles k = 1 .. G-1 of the cross-wave stages, [set][fwd/inv][k]
 __constant__ uint2 c_cross[LARGE_NPS][2][4];
-// last sub-tree inverse stage: n^-1 psi^-brv(2^g + B), centred signed pair
-__constant__ uint2 c_lastinv[LARGE_NPS][LARGE_GMAX];
+// last sub-tree inverse stage: n^-1 psi^-brv(2^g + B), centred signed pair,
+// [set][plain / times 2^32 (the products' Montgomery factor)][B]
+__constant__ uint2 c_lastinv[LARGE_NPS][2][LARGE_GMAX];
 // LDS images (lane twiddles + bit-5 table) of T_B, [set][fwd/inv][B]; the
 // kernels copy the lane twiddles of B = 0 only (shared, see c_fscale) and the
 // 32-entry bit-5 table of every B
@@ -62,7 +63,7 @@ __device__ uint4 g_tw2imgL[LARGE_NPS][2][LARGE_GMAX][TW2_VEC4];
 // 15.75 KiB LDS images (n = 8192) are freed: 16 waves per workgroup instead of 12.
 __constant__ uint2 c_fscale[LARGE_NPS][2][LARGE_GMAX][32];
 
-template <int PS>
+template <int PS, int MULW = 0>
 struct Large {
     using PL = typename PSel<PS>::T;   // the n-point set
     using P = PS2;                     // 2048-point sub-transforms over the same prime
@@ -75,15 +76,21 @@ struct Large {
     // share T_0's lane table and scale by c_fscale (SHARED): 4.94 / 4.75 ->
     // 4.62 / 4.59 ms fwd / inv per 2^18 polys, while at n = 4096 the scaling
     // only costs (3.98 / 3.97 -> 4.20 / 4.04 ms), profiles/r03/ab_l*_tab.log
-    static constexpr int WAVES = 16;
-    static constexpr bool SHARED = G == 4;
+    // The fused products (MULW = their waves per workgroup) hold one
+    // operand's 32 transformed words through the other's transform: 12 waves
+    // at 3 per SIMD (168 VGPRs) or 8 at 2 (256), both directions' tables in
+    // LDS, always the shared lane table.
+    static constexpr bool MUL = MULW != 0;
+    static constexpr int WAVES = MUL ? MULW : 16;
+    static constexpr bool SHARED = MUL || G == 4;
     static constexpr int OCC = WAVES / 4;
     static constexpr int SLOTS = WAVES / G;   // polynomials per workgroup step
     static constexpr int NT = WAVES * 64;
     static constexpr int IDX = PS - LARGE_PS0;
     // lane tables (shared: T_0's + per-B bit-5 tables; else G whole images)
     static constexpr int TAB_WORDS = SHARED ? TW2_WORDS + G * 64 : G * TW2_WORDS;
-    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + TAB_WORDS + SLOTS + 1;   // + slot counters, poison word
+    static constexpr int NTAB = MUL ? 2 : 1;   // forward table, then (MUL) the inverse's
+    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + NTAB * TAB_WORDS + SLOTS + 1;   // + slot counters, poison word
 };
 
 // global-order offset of sub-block B's outputs: brv_g(B)
@@ -218,13 +225,13 @@ __device__ __forceinline__ uint32_t xch_pos(uint32_t kp, uint32_t B)
     return (kp + B * (32u / G)) & 2047u;
 }
 
-// The workgroup's twiddle tables of one direction into LDS after the
-// transpose buffers: T_0's lane image, then the bit-5 table of every B.
+// The workgroup's twiddle tables of one direction into LDS at `tab`: T_0's
+// lane image, then the bit-5 table of every B (SHARED), else the G images.
 constexpr int TW2_BIT5_VEC4 = TW2_ENTRIES * 64 * 2 / 4;   // uint4 offset of the bit-5 table in an image
 template <class LG, bool INV>
-__device__ __forceinline__ void fill_large_tw(uint32_t *lds)
+__device__ __forceinline__ void fill_large_tw(uint32_t *tab)
 {
-    uint4 *dst = reinterpret_cast<uint4 *>(lds + LG::WAVES * XPOSE_WORDS);
+    uint4 *dst = reinterpret_cast<uint4 *>(tab);
     if constexpr (!LG::SHARED) {   // the G images, contiguous in g_tw2imgL
         const uint4 *src = g_tw2imgL[LG::IDX][INV ? 1 : 0][0];
         for (int i = threadIdx.x; i < LG::G * TW2_VEC4; i += LG::NT) dst[i] = src[i];
@@ -248,10 +255,153 @@ __device__ __forceinline__ void subtree_scale(uint32_t (&r)[32], uint32_t B)
     for (int j = 0; j < 32; ++j) r[j] = shoup_mul<P::Q>(r[j], f[j].x, f[j].y);
 }
 
+// Per-wave state of the large-n kernels: the wave's sub-block B and slot,
+// its exchange buffer, the slot barrier and, per direction, the lane table
+// (T_0's when SHARED, else T_B's image) and T_B's bit-5 table.
+template <class LG>
+struct LargeWave {
+    using P = typename LG::P;
+    using LT = Lane<P>;
+    uint32_t *lds, *buf;
+    uint32_t wave, B, slot;
+    const uint2 *tw2[2], *bit5[2];
+    SlotSync ss;
+    LT L;
+    // fills the tables of directions [D0, D1] and the counters (one __syncthreads)
+    template <int D0, int D1>
+    __device__ __forceinline__ void init(uint32_t *lds_)
+    {
+        lds = lds_;
+        wave = wave_id();
+        B = wave % LG::G;
+        slot = wave / LG::G;
+        buf = lds + wave * XPOSE_WORDS;
+        uint32_t *tab = lds + LG::WAVES * XPOSE_WORDS;
+        if constexpr (D0 == 0) table<0>(tab);
+        if constexpr (D1 == 1) table<1>(tab + (D0 == 0 ? LG::TAB_WORDS : 0));
+        uint32_t *const ctrs = tab + LG::NTAB * LG::TAB_WORDS;
+        if (threadIdx.x <= (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;   // slot counters + poison word
+        __syncthreads();
+        ss = SlotSync{ctrs + slot, ctrs + LG::SLOTS, 0};
+    }
+    template <int D>
+    __device__ __forceinline__ void table(uint32_t *t)
+    {
+        tw2[D] = reinterpret_cast<const uint2 *>(t + (LG::SHARED ? 0u : B * TW2_WORDS));
+        bit5[D] = LG::SHARED ? reinterpret_cast<const uint2 *>(t + TW2_BIT5_VEC4 * 4 + B * 64) : tw2[D] + TW2_ENTRIES * 64;
+        fill_large_tw<LG, D == 1>(t);
+    }
+    __device__ __forceinline__ const uint32_t *partner(uint32_t d) const { return lds + (wave ^ d) * XPOSE_WORDS; }
+
+    // forward of this wave's share (sub-block B words 2048 B + p', inputs
+    // < 2q at register j of lane l = p' 64 j + brl) down to the pass-2
+    // layout: register j of lane l holds sub-block output k' = brv5(j) 64 + l
+    // of global index G k' + brv_g(B), in [0,4q)
+    __device__ __forceinline__ void fwd(uint32_t (&r)[32])
+    {
+        constexpr int G = LG::G;
+        constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1), then for n = 8192 pos bit 11 (k = 2 + B/2)
+        cross_ct<P, false, G>(r, buf, partner(D0), opaque_lane(), (B & D0) != 0, c_cross[LG::IDX][0][1], ss);
+        if constexpr (G == 4)
+            cross_ct<P, true, G>(r, buf, partner(1u), opaque_lane(), (B & 1u) != 0, c_cross[LG::IDX][0][2 + (B >> 1)], ss);
+        fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), bit5[0] + opaque_zero());
+        lds_p1_to_p2<P>(r, buf, LT(opaque_lane()));   // addresses recomputed (see inv)
+        subtree_scale<P, LG, false>(r, B);             // T_B = c_{B,b} T_0 (c_fscale)
+        fwd_pass2<P>(r, tw2[0] + opaque_zero(), L.lane);
+    }
+    // all-to-all through the exchange buffers: from the pass-2 layout to
+    // global words [2048 B, 2048 B + 2048) at register j of lane l = word
+    // 64 j + l (lane-contiguous runs), canonical
+    __device__ __forceinline__ void to_contiguous(uint32_t (&r)[32])
+    {
+        constexpr int G = LG::G;
+        const uint32_t lane = opaque_lane();   // addresses recomputed per step, not hoisted into VGPRs
+#pragma unroll
+        for (int j = 0; j < 32; ++j) buf[xch_pos<G>(brv5(j) * 64 + lane, B)] = canon4<P>(r[j]);
+        ss.template wait<G>();
+        {
+            const uint32_t bs = brv_g(lane % G, LG::LOGG);   // source wave of global word g (g = lane mod G)
+            const uint32_t *src = lds + (slot * G + bs) * XPOSE_WORDS;
+            const uint32_t k0 = 2048u / G * B + lane / G;     // k' of j = 0
+#pragma unroll
+            for (int j = 0; j < 32; ++j) r[j] = src[xch_pos<G>(k0 + 64u / G * j, bs)];
+        }
+        ss.template wait<G>();   // the buffers are free for the next exchanges
+    }
+    // the inverse of to_contiguous (no reduction): contiguous words scattered
+    // to the owning waves, back in the pass-2 layout (the buffers must be free)
+    __device__ __forceinline__ void from_contiguous(uint32_t (&r)[32])
+    {
+        constexpr int G = LG::G;
+        const uint32_t lane = opaque_lane();   // (see to_contiguous)
+        {
+            const uint32_t bt = brv_g(lane % G, LG::LOGG);   // owner of g (g = lane mod G)
+            uint32_t *dst = lds + (slot * G + bt) * XPOSE_WORDS;
+            const uint32_t k0 = 2048u / G * B + lane / G;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) dst[xch_pos<G>(k0 + 64u / G * j, bt)] = r[j];
+        }
+        ss.template wait<G>();
+#pragma unroll
+        for (int j = 0; j < 32; ++j) r[j] = buf[xch_pos<G>(brv5(j) * 64 + lane, B)];
+    }
+    // inverse from the pass-2 layout (inputs < 2q) to this wave's share of
+    // the natural order (word 2048 B + 64 j + brl at register j), [0,2q),
+    // scaled by n^-1 (RS: and by 2^32, undoing a Montgomery product's 2^-32)
+    template <bool RS>
+    __device__ __forceinline__ void inv(uint32_t (&r)[32])
+    {
+        constexpr int G = LG::G;
+        constexpr uint32_t NINV = RS ? LG::PL::NINV_R : LG::PL::NINV;
+        constexpr uint32_t NINVP = cshoup(NINV, P::Q);
+        inv_pass2<P>(r, tw2[1] + opaque_zero(), L.lane);
+        subtree_scale<P, LG, true>(r, B);   // the c'_{B,b} the shared table left out (c_fscale)
+        // transpose addresses from an opaque lane: recomputed here instead of
+        // 8 loop-invariant VGPRs (which spilled at the 128-VGPR budget)
+        lds_p2_to_p1<P>(r, buf, LT(opaque_lane()));
+        inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5[1] + opaque_zero());
+        const uint2 last = c_lastinv[LG::IDX][RS ? 1 : 0][B];
+        inv_last_stage<P, false>(r, NINV, NINVP, last.x, last.y);   // [0,2q)
+        if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)
+            cross_gs<P, G>(r, buf, partner(1u), opaque_lane(), (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)], ss);
+        constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1)
+        cross_gs<P, G>(r, buf, partner(D0), opaque_lane(), (B & D0) != 0, c_cross[LG::IDX][1][1], ss);
+    }
+};
+
 // Workgroup b owns polynomials [b SLOTS ppw, (b+1) SLOTS ppw); slot s of a
 // step takes waves s G .. s G + G-1.  Every wave runs the workgroup's step
 // count (the exchanges hold barriers): slots past the batch recompute the
-// workgroup's first polynomial and store nothing.
+// workgroup's first polynomial and store nothing.  step(base, valid): base =
+// the wave's first global word (uniform); the steps add the lane offset as
+// opaque_lane() at every load and store, so the accesses keep the scalar
+// base + 32-bit offset form and no 64-bit lane address stays live (or is
+// hoisted out of the loop into VGPRs).
+template <class LG, class Step>
+__device__ __forceinline__ void large_steps(const LargeWave<LG> &w, uint32_t first, uint32_t npoly, uint32_t ppw, Step &step)
+{
+    const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
+#pragma unroll 1
+    for (uint32_t it = 0; it < steps; ++it) {
+        const uint32_t poly = first + it * LG::SLOTS + w.slot;
+        const bool valid = poly < npoly;
+        step((size_t)(valid ? poly : first) * LG::PL::N + w.B * 2048u, valid);
+    }
+}
+
+// the step's stores: a poisoned workgroup (expired slot barrier) writes sentinels
+template <class LG, class F>
+__device__ __forceinline__ void large_store(uint32_t *dst, const LargeWave<LG> &w, F val)
+{
+    const bool bad = w.ss.poisoned();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, bad ? SYNC_SENTINEL : val(j));
+}
+
+// The standalone transforms keep their own step bodies (the same dataflow as
+// LargeWave::fwd / to_contiguous and from_contiguous / inv): written through
+// the shared helpers, the inverse's schedule spilled 13-15 VGPRs at the
+// 128-VGPR budget of 16 waves per workgroup.
 template <int PS>
 __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large(const uint32_t *in, uint32_t *out,
                                                                                 uint32_t npoly, uint32_t ppw)
@@ -270,7 +420,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
     const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + (LG::SHARED ? 0u : B * TW2_WORDS));
     const uint2 *bit5 = LG::SHARED ? reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + TW2_BIT5_VEC4 * 4 + B * 64)
                                    : tw2 + TW2_ENTRIES * 64;
-    fill_large_tw<LG, false>(lds);
+    fill_large_tw<LG, false>(lds + LG::WAVES * XPOSE_WORDS);
     uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + LG::TAB_WORDS;
     if (threadIdx.x <= (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;   // slot counters + poison word
     __syncthreads();
@@ -339,7 +489,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
     const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + (LG::SHARED ? 0u : B * TW2_WORDS));
     const uint2 *bit5 = LG::SHARED ? reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + TW2_BIT5_VEC4 * 4 + B * 64)
                                    : tw2 + TW2_ENTRIES * 64;
-    fill_large_tw<LG, true>(lds);
+    fill_large_tw<LG, true>(lds + LG::WAVES * XPOSE_WORDS);
     uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + LG::TAB_WORDS;
     if (threadIdx.x <= (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;   // slot counters + poison word
     __syncthreads();
@@ -374,7 +524,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
         // 8 loop-invariant VGPRs (which spilled at the 128-VGPR budget)
         lds_p2_to_p1<P>(r, buf, LT(opaque_lane()));
         inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5 + opaque_zero());
-        const uint2 last = c_lastinv[LG::IDX][B];
+        const uint2 last = c_lastinv[LG::IDX][0][B];
         inv_last_stage<P, false>(r, LG::PL::NINV, NINVP, last.x, last.y);   // [0,2q), scaled by n^-1
         if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)
             cross_gs<P, G>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)], ss);
@@ -385,6 +535,94 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
             uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
 #pragma unroll
             for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, bad ? SYNC_SENTINEL : csub<P::Q>(r[j]));
+        }
+    }
+}
+
+#ifndef MUL_PF
+#define MUL_PF 1
+#endif
+// Fused product c = a*b mod (x^n + 1) for n = 4096 / 8192: FWD(a) and FWD(b)
+// (or b-hat = poly_ntt(b), natural order, brought to the pass-2 layout by the
+// contiguous-load scatter: BHAT) meet in the pass-2 layout, where the
+// pointwise Montgomery product is taken; the inverse starts from there (its
+// n^-1 scaling carries the 2^32) -- the two forward exchanges and the
+// inverse's scatter of a separate pipeline never happen, one HBM read of a
+// and b, one write of c.  a, b and c may alias: the G waves of a slot load
+// all of a and b before the slot barriers that precede any store.
+#ifndef MUL_LARGE_WAVES
+#define MUL_LARGE_WAVES 8   // n = 8192 product with both operands transformed: 8 waves at 2 per
+                             // SIMD (199 VGPRs) 6.68 ms vs 12 at 3 (37 VGPRs spilled) 6.77 ms per
+                             // 2^17 products (profiles/r03/ab_mul_large.log)
+#endif
+template <int PS, bool BHAT>
+constexpr int mul_large_waves()
+{
+    return (PSel<PS>::T::N == 8192 && !BHAT) ? MUL_LARGE_WAVES : 12;
+}
+template <int PS, bool BHAT>
+__global__ __launch_bounds__((Large<PS, mul_large_waves<PS, BHAT>()>::NT), (Large<PS, mul_large_waves<PS, BHAT>()>::OCC))
+void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
+{
+    using LG = Large<PS, mul_large_waves<PS, BHAT>()>;
+    using P = typename LG::P;
+    constexpr bool PF = MUL_PF;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
+    const uint32_t first = blockIdx.x * (LG::SLOTS * ppw);
+    if (first >= npoly) return;
+    LargeWave<LG> w;
+    w.template init<0, 1>(lds);
+    auto step = [&](size_t base, bool valid) {
+        uint32_t ra[32], rb[32];
+        // both operands' loads issued up front: b's latency hides behind a's
+        // transform (its 32 words are live there either way, as a's are
+        // through b's transform)
+        load32(ra, a + base + opaque_lane(), [](int j) { return 64 * j; });
+        if (PF) load32(rb, b + base + opaque_lane(), [](int j) { return 64 * j; });
+        w.fwd(ra);
+        if (!PF) load32(rb, b + base + opaque_lane(), [](int j) { return 64 * j; });
+        if constexpr (BHAT) {   // b-hat < 2q
+            // the scatter writes the partners' buffers: their forward
+            // transposes (lds_p1_to_p2 on their own buffers) must be done
+            w.ss.template wait<LG::G>();
+            w.from_contiguous(rb);
+        }
+        else w.fwd(rb);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(csub<P::Q2>(ra[j]), csub<P::Q2>(rb[j]));
+        w.template inv<true>(ra);
+        if (valid) large_store(c + base + opaque_lane(), w, [&](int j) { return csub<P::Q>(ra[j]); });
+    };
+    large_steps(w, first, npoly, ppw, step);
+}
+
+// out[t] = in[brv_L(t)] for n = 4096 / 8192 (L = log2 n), any 32-bit words:
+// one 512-thread workgroup per polynomial, coalesced dword loads into LDS at
+// swz(p) = p ^ ((p >> (L-5)) & 31), coalesced dword stores read from
+// swz(brv(t)).  32 consecutive s (writes) share the XOR term and differ in
+// the bank bits; 32 consecutive t (reads) differ only in bits L-1 .. L-5 of
+// brv(t), which the XOR term moves into the bank bits: conflict-free both ways.
+template <int PS>
+__global__ __launch_bounds__(512) void k_bitrev_large(const uint32_t *in, uint32_t *out, uint32_t npoly)
+{
+    constexpr uint32_t N = PSel<PS>::T::N;
+    constexpr int LOGN = PSel<PS>::T::LOGN;
+    __shared__ uint32_t x[N];
+    auto swz = [](uint32_t p) { return p ^ ((p >> (LOGN - 5)) & 31u); };
+#pragma unroll 1
+    for (uint32_t poly = blockIdx.x; poly < npoly; poly += gridDim.x) {   // in place: all loads before any store
+        const size_t base = (size_t)poly * N;
+        uint32_t v[N / 512];
+#pragma unroll
+        for (uint32_t k = 0; k < N / 512; ++k) v[k] = __builtin_nontemporal_load(in + base + 512 * k + threadIdx.x);
+        __syncthreads();   // the previous polynomial's reads of x are done
+#pragma unroll
+        for (uint32_t k = 0; k < N / 512; ++k) x[swz(512 * k + threadIdx.x)] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < N / 512; ++k) {
+            const uint32_t t = 512 * k + threadIdx.x;
+            __builtin_nontemporal_store(x[swz(__builtin_bitreverse32(t) >> (32 - LOGN))], out + base + t);
         }
     }
 }

@@ -35,7 +35,8 @@ def test_error_codes_before_any_gpu_work(ntt):
     L = ntt.lib()
     fake = 0x10000  # never dereferenced: validation fails first
     assert L.poly_ntt(fake, None, 1, 5, None) == ntt.NTT_ERR_PARAM
-    assert L.poly_mul(fake, fake, fake, 1, 3, None) == ntt.NTT_ERR_PARAM      # no fused product at n > 2048
+    assert L.poly_mul_nussbaumer(fake, fake, fake, 1, 3, 0, None) == ntt.NTT_ERR_PARAM   # no Nussbaumer split at n > 2048
+    assert L.poly_mul(fake + 8, fake, fake + 0x100000, 1, 3, None) == ntt.NTT_ERR_ALIAS   # n = 4096 product: checked
     assert L.poly_ntt(None, None, 1, 0, None) == ntt.NTT_ERR_NULL
     assert L.poly_ntt(fake + 2, None, 1, 0, None) == ntt.NTT_ERR_ALIGN
     assert L.poly_ntt(None, None, 0, 0, None) == ntt.NTT_OK      # empty batch is a no-op

@@ -91,23 +91,134 @@ def test_large_polymul_composition(ntt, oracle, dev, ps):
     assert np.array_equal(c[4], ((2 * np.arange(n) + 2 - n) % q).astype(np.uint32))
 
 
-def test_large_unsupported_ops(ntt, dev):
-    """Bit-reversed orders, the fused product and Nussbaumer exist for n <= 2048
-    only: NTT_ERR_PARAM, nothing launched."""
+def test_large_nussbaumer_unsupported(ntt, dev):
+    """Nussbaumer splits n = 1024 / 2048 only (the reference's routine is
+    n = 1024): NTT_ERR_PARAM for the large sets, nothing launched."""
     L = ntt.lib()
     for ps in (3, 4):
         n = ntt.param_info(ps)["n"]
         t = torch.zeros(2 * n, dtype=torch.int32, device=dev)
         u = torch.zeros_like(t)
         p, q = t.data_ptr(), u.data_ptr()
-        assert L.poly_ntt_bitrev(q, p, 2, ps, None) == ntt.NTT_ERR_PARAM
-        assert L.poly_invntt_bitrev(q, p, 2, ps, None) == ntt.NTT_ERR_PARAM
-        assert L.poly_bitrev_copy(q, p, 2, ps, None) == ntt.NTT_ERR_PARAM
-        assert L.poly_mul(q, p, p, 2, ps, None) == ntt.NTT_ERR_PARAM
-        assert L.poly_mul_ntt(q, p, p, 2, ps, None) == ntt.NTT_ERR_PARAM
         assert L.poly_mul_nussbaumer(q, p, p, 2, ps, 0, None) == ntt.NTT_ERR_PARAM
         assert L.poly_ntt(p, None, 0, ps, None) == 0
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+@pytest.mark.parametrize("batch", [1, 2, 5, 7, 64, 389])
+def test_large_poly_mul_random(ntt, oracle, dev, ps, batch):
+    """Fused product (k_poly_mul_large): partial and full workgroup steps
+    (SLOTS = 6 / 2 polynomials per step), bit-exact against the oracle."""
+    a = oracle.fill_uniform(batch, ps, 0x3A + batch, 0)
+    b = oracle.fill_uniform(batch, ps, 0x3B + batch, 0)
+    ta, tb = _dev(ntt, a, dev), _dev(ntt, b, dev)
+    tc = torch.empty_like(ta)
+    ntt.poly_mul(tc, ta, tb, ps)
+    want = oracle.poly_mul(a, b, ps)
+    assert np.array_equal(_u32(ntt, tc), want)
+    assert np.array_equal(_u32(ntt, ta), a) and np.array_equal(_u32(ntt, tb), b)
+    # b-hat = poly_ntt(b): the second operand already in the NTT domain
+    tbh = _dev(ntt, b, dev)
+    ntt.poly_ntt(tbh, ps)
+    tc2 = torch.empty_like(ta)
+    ntt.poly_mul_ntt(tc2, ta, tbh, ps)
+    assert np.array_equal(_u32(ntt, tc2), want)
+    torch.cuda.synchronize()
+    assert ntt.sync_expiries() == 0
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+def test_large_poly_mul_kat_aliasing_lazy(ntt, oracle, dev, ps):
+    """All-ones KAT z[k] = 2k + 2 - n mod q (NTT.cu:2360, 2433-2438), the
+    init_operand pattern (NTT.cu:10-15), c aliasing a / b / both, inputs in
+    [q, 2q) and edge operands."""
+    n, q = ntt.param_info(ps)["n"], ntt.param_info(ps)["q"]
+    ones = np.ones((1, n), np.uint32)
+    t1 = _dev(ntt, ones, dev)
+    tc = torch.empty_like(t1)
+    ntt.poly_mul(tc, t1, t1, ps)
+    assert np.array_equal(_u32(ntt, tc)[0], ((2 * np.arange(n) + 2 - n) % q).astype(np.uint32))
+    pat = np.zeros((1, n), np.uint32)
+    pat[0, : n // 2] = n // 2 - np.arange(n // 2)
+    tp = _dev(ntt, pat, dev)
+    ntt.poly_mul(tc, tp, tp, ps)
+    assert np.array_equal(_u32(ntt, tc), oracle.poly_mul(pat, pat, ps))
+
+    a = oracle.fill_uniform(9, ps, 0xA1, 0)
+    b = oracle.fill_uniform(9, ps, 0xB1, 0)
+    a[0] = 0
+    b[1] = q - 1
+    a[2] = np.eye(1, n, n - 1, dtype=np.uint32)[0]   # x^(n-1): negacyclic wrap
+    b[2] = np.eye(1, n, 1, dtype=np.uint32)[0]
+    want = oracle.poly_mul(a, b, ps)
+    assert np.array_equal(want[2], ((q - 1) * np.eye(1, n, 0, dtype=np.uint64)[0] % q).astype(np.uint32))
+    for alias in ("a", "b"):
+        ta, tb = _dev(ntt, a, dev), _dev(ntt, b, dev)
+        out = ta if alias == "a" else tb
+        ntt.poly_mul(out, ta, tb, ps)
+        assert np.array_equal(_u32(ntt, out), want), alias
+    ta = _dev(ntt, a, dev)
+    ntt.poly_mul(ta, ta, ta, ps)
+    assert np.array_equal(_u32(ntt, ta), oracle.poly_mul(a, a, ps))
+    al = (a.astype(np.uint64) + q).astype(np.uint32)
+    bl = (b.astype(np.uint64) + q).astype(np.uint32)
+    ta, tb = _dev(ntt, al, dev), _dev(ntt, bl, dev)
+    tc = torch.empty_like(ta)
+    ntt.poly_mul(tc, ta, tb, ps)
+    assert np.array_equal(_u32(ntt, tc), want)
+    # b-hat with entries in [q, 2q) (the forward's lazy range is allowed)
+    bh = (oracle.poly_ntt(b, ps).astype(np.uint64) + q).astype(np.uint32)
+    tbh = _dev(ntt, bh, dev)
+    ta = _dev(ntt, a, dev)
+    ntt.poly_mul_ntt(tbh, ta, tbh, ps)
+    assert np.array_equal(_u32(ntt, tbh), want)
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+def test_large_bit_reversed_orders(ntt, oracle, dev, ps):
+    """poly_bitrev_copy (bit_reverse_copy_tbl_gpu, NTT.cu:487-492) at
+    log2 n = 12 / 13 bits, in and out of place; poly_ntt_bitrev =
+    bitrev(poly_ntt); poly_invntt_bitrev on bit-reversed input = the CT
+    inverse (oracle_poly_invntt_ct) = poly_invntt."""
+    for batch in (1, 3, 130):
+        x = oracle.fill_uniform(batch, ps, 0xB17 + batch, 0)
+        tx = _dev(ntt, x, dev)
+        ty = torch.empty_like(tx)
+        ntt.poly_bitrev_copy(ty, tx, ps)
+        assert np.array_equal(_u32(ntt, ty), oracle.bit_reverse_copy(x, ps))
+        ntt.poly_bitrev_copy(ty, ty, ps)   # an involution, in place
+        assert np.array_equal(_u32(ntt, ty), x)
+        X = oracle.poly_ntt(x, ps)
+        ntt.poly_ntt_bitrev(ty, tx, ps)
+        assert np.array_equal(_u32(ntt, ty), oracle.bit_reverse_copy(X, ps))
+        assert np.array_equal(_u32(ntt, tx), x)
+        ntt.poly_ntt_bitrev(tx, tx, ps)
+        assert np.array_equal(_u32(ntt, tx), oracle.bit_reverse_copy(X, ps))
+        Xb = oracle.bit_reverse_copy(X, ps)
+        tX = _dev(ntt, Xb, dev)
+        ntt.poly_invntt_bitrev(ty, tX, ps)
+        assert np.array_equal(_u32(ntt, ty), x)
+        ntt.poly_invntt_bitrev(tX, tX, ps)
+        assert np.array_equal(_u32(ntt, tX), x)
+        # an arbitrary bit-reversed-order vector vs the oracle's CT inverse
+        # (oracle_poly_invntt_ct takes natural order and bit-reverses itself)
+        Ybr = oracle.fill_uniform(batch, ps, 0xB18 + batch, 0)
+        tY = _dev(ntt, Ybr, dev)
+        ntt.poly_invntt_bitrev(tY, tY, ps)
+        assert np.array_equal(_u32(ntt, tY), oracle.poly_invntt_ct(oracle.bit_reverse_copy(Ybr, ps), ps))
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+def test_large_poly_mul_host(ntt, oracle, ps):
+    """poly_mul_host through the streamed host context at n = 4096 / 8192
+    (ragged last chunk)."""
+    a = oracle.fill_uniform(37, ps, 0x40, 0)
+    b = oracle.fill_uniform(37, ps, 0x41, 0)
+    c = np.empty_like(a)
+    with ntt.HostContext(ps, chunk_polys=16, nslots=2) as h:
+        h.mul(c, a, b)
+    assert np.array_equal(c, oracle.poly_mul(a, b, ps))
 
 
 @pytest.mark.slow
@@ -150,6 +261,9 @@ def test_large_slot_barriers_never_expire(ntt, oracle, dev, ps):
         ntt.poly_ntt(x, ps)
         ntt.poly_invntt(x, ps)
         assert torch.equal(x, ref)
+        y = torch.empty_like(x)
+        ntt.poly_mul(y, x, x, ps)
+        ntt.poly_mul_ntt(y, x, y, ps)
     torch.cuda.synchronize()
     assert ntt.sync_expiries() == 0
 
@@ -171,6 +285,7 @@ def test_large_expired_slot_barrier_writes_sentinel(ntt, dev, ps):
     vp, sz = ctypes.c_void_p, ctypes.c_size_t
     L.poly_ntt.argtypes = [vp, vp, sz, ctypes.c_int, vp]
     L.poly_invntt.argtypes = [vp, vp, sz, ctypes.c_int, vp]
+    L.poly_mul.argtypes = [vp, vp, vp, sz, ctypes.c_int, vp]
     L.ntt_sync_expiries.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
     psn = ntt.PARAM_SETS[ps]
     n = ntt.param_info(ps)["n"]
@@ -181,6 +296,13 @@ def test_large_expired_slot_barrier_writes_sentinel(ntt, dev, ps):
         assert fn(x.data_ptr(), None, 37, psn, None) == 0
         torch.cuda.synchronize()
         assert bool((x == -1).all()), "expired waits must write the sentinel everywhere"
+    x = torch.empty(37 * n, dtype=torch.int32, device=dev)
+    ntt.fill_uniform(x, ps, 0x5E18, 0)
+    y = torch.zeros_like(x)
+    torch.cuda.synchronize()
+    assert L.poly_mul(y.data_ptr(), x.data_ptr(), x.data_ptr(), 37, psn, None) == 0
+    torch.cuda.synchronize()
+    assert bool((y == -1).all()), "the fused product fails loudly too"
     c = ctypes.c_uint32(0)
     assert L.ntt_sync_expiries(ctypes.byref(c)) == 0
     assert c.value > 0
