@@ -249,6 +249,35 @@ def test_large_full_batch_properties(ntt, oracle, dev, ps, batch):
     assert torch.equal(lhs, s.to(torch.int64) & 0xFFFFFFFF)
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("ps,batch", [("p-III-4096", (1 << 18) + 5), ("p-III-8192", (1 << 17) + 1)])
+def test_large_poly_mul_full_batch_properties(ntt, oracle, dev, ps, batch):
+    """3 x 4-GiB operands: sampled products vs the oracle, commutativity over
+    the whole batch, poly_mul_ntt(a, NTT(b)) == poly_mul(a, b) on the whole
+    batch, no expired slot barrier."""
+    n = ntt.param_info(ps)["n"]
+    a = torch.empty(batch * n, dtype=torch.int32, device=dev)
+    b = torch.empty_like(a)
+    ntt.fill_uniform(a, ps, 0x5EED0011, 0)
+    ntt.fill_uniform(b, ps, 0x5EED0012, 0)
+    c = torch.empty_like(a)
+    ntt.poly_mul(c, a, b, ps)
+    rng = np.random.default_rng(5)
+    idx = np.unique(np.concatenate([[0, batch - 1], rng.integers(0, batch, 30)]))
+    sel = torch.as_tensor(idx, device=dev)
+    A = ntt.to_numpy_u32(a.view(batch, n)[sel])
+    B = ntt.to_numpy_u32(b.view(batch, n)[sel])
+    assert np.array_equal(ntt.to_numpy_u32(c.view(batch, n)[sel]), oracle.poly_mul(A, B, ps))
+    d = torch.empty_like(a)
+    ntt.poly_mul(d, b, a, ps)
+    assert torch.equal(c, d)
+    ntt.poly_ntt(b, ps)          # b-hat, in place
+    ntt.poly_mul_ntt(d, a, b, ps)
+    assert torch.equal(c, d)
+    torch.cuda.synchronize()
+    assert ntt.sync_expiries() == 0
+
+
 @pytest.mark.parametrize("ps", LARGE_SETS)
 def test_large_slot_barriers_never_expire(ntt, oracle, dev, ps):
     """The per-polynomial barriers' bounded waits (SlotSync) never run out,

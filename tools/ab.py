@@ -37,7 +37,7 @@ def main():
     libs = {}
     for path in args.libs:
         L = ctypes.CDLL(os.path.abspath(path))
-        for nm in ("poly_ntt_oop", "poly_invntt_oop"):
+        for nm in ("poly_ntt_oop", "poly_invntt_oop", "poly_bitrev_copy", "poly_ntt_bitrev", "poly_invntt_bitrev"):
             getattr(L, nm).argtypes = [vp, vp, sz, ctypes.c_int, vp]
         L.poly_mul.argtypes = [vp, vp, vp, sz, ctypes.c_int, vp]
         L.poly_mul_ntt.argtypes = [vp, vp, vp, sz, ctypes.c_int, vp]
@@ -57,6 +57,9 @@ def main():
             rc = L.poly_ntt_oop(dst.data_ptr(), x.data_ptr(), args.batch, ps, s.cuda_stream)
         elif op == "inv":
             rc = L.poly_invntt_oop(dst.data_ptr(), x.data_ptr(), args.batch, ps, s.cuda_stream)
+        elif op in ("bitrev", "fwdbr", "invbr"):
+            fn = {"bitrev": L.poly_bitrev_copy, "fwdbr": L.poly_ntt_bitrev, "invbr": L.poly_invntt_bitrev}[op]
+            rc = fn(dst.data_ptr(), x.data_ptr(), args.batch, ps, s.cuda_stream)
         elif op in ("nus", "nusm32"):
             rc = L.poly_mul_nussbaumer(z.data_ptr(), x.data_ptr(), y.data_ptr(), args.batch, ps, 1 if op == "nusm32" else 0,
                                        s.cuda_stream)
@@ -72,7 +75,7 @@ def main():
         for op in ops:
             launch(L, op)
             torch.cuda.synchronize()
-            sig = (x if args.inplace and op in ("fwd", "inv") else z)[:: 4099].clone()
+            sig = (x if args.inplace and op in ("fwd", "inv", "bitrev", "fwdbr", "invbr") else z)[:: 4099].clone()
             if op not in ref:
                 ref[op] = sig
             ok[f"{name}:{op}"] = bool(torch.equal(ref[op], sig))

@@ -61,6 +61,14 @@ for step in "$@"; do
                 run pmcl_${n}_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcl_${n}_fetch -o run -- python3 bench.py $a &&
                 run pmcl_${n}_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcl_${n}_write -o run -- python3 bench.py $a &&
                 run pmcl_${n}_sum 60 python3 tools/pmc_summary.py --op fwdinv --param p-III-$n --batch $b --fetch gpurun_out/pmcl_${n}_fetch/run_counter_collection.csv --write gpurun_out/pmcl_${n}_write/run_counter_collection.csv --out gpurun_out/pmc_summary.json ;;
+        pmcm_*) n=${step#pmcm_}; b=$((1073741824 / n)); a="--op polymul --param p-III-$n --batch $b --steps 3 --warmup 1 --no-cpu-baseline --no-check";
+                run pmcm_${n}_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcm_${n}_fetch -o run -- python3 bench.py $a &&
+                run pmcm_${n}_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcm_${n}_write -o run -- python3 bench.py $a &&
+                run pmcm_${n}_sum 60 python3 tools/pmc_summary.py --op polymul --param p-III-$n --batch $b --fetch gpurun_out/pmcm_${n}_fetch/run_counter_collection.csv --write gpurun_out/pmcm_${n}_write/run_counter_collection.csv --out gpurun_out/pmc_summary.json ;;
+        benchm_*) n=${step#benchm_}; b=$((1073741824 / n)); run benchm_$n 300 python bench.py --op polymul --param p-III-$n --batch $b --steps 20 --warmup 3 --cpu-seconds 5 &&
+                  run benchmn_$n 300 python bench.py --op polymul_ntt --param p-III-$n --batch $b --steps 20 --warmup 3 --cpu-seconds 5 ;;
+        profm_*) n=${step#profm_}; b=$((1073741824 / n)); run profm_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profm_$n -o run -- python3 bench.py --op polymul --param p-III-$n --batch $b --steps 20 --warmup 3 --no-cpu-baseline --no-check ;;
+        profl_*) n=${step#profl_}; b=$((8589934592 / 4 / n)); run profl_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profl_$n -o run -- python3 bench.py --op fwdinv --param p-III-$n --batch $b --steps 20 --warmup 3 --no-cpu-baseline --no-check ;;
         benchl_*) n=${step#benchl_}; b=$((8589934592 / 4 / n)); run benchl_$n 300 python bench.py --op fwdinv --param p-III-$n --batch $b --steps 20 --warmup 3 --cpu-seconds 5 ;;
         sq_c*) c=${step#sq_c}; run sq_c$c 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sq_c$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-check ;;
         sqb_c*) c=${step#sqb_c}; run sqb_c$c 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM --output-format csv -d gpurun_out/sqb_c$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-check ;;
