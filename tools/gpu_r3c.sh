@@ -12,5 +12,4 @@ cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_mul4096 -o run -- python3 bench.py --op polymul --param p-III-4096 --batch 262144 --steps 10 --warmup 2 --no-cpu-baseline --no-check > $O/prof_mul4096.log 2>&1 || exit 1
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_mul8192 -o run -- python3 bench.py --op polymul --param p-III-8192 --batch 131072 --steps 10 --warmup 2 --no-cpu-baseline --no-check > $O/prof_mul8192.log 2>&1 || exit 1
 
-timeout -k 10 60 ntt-gpu-qtesla_amd/bin/valu_rate > gpurun_out/r3c/valu_rate.log 2>&1 || exit 1; cat gpurun_out/r3c/valu_rate.log
 echo done
