@@ -15,7 +15,9 @@
 //                 reference's PCIe-inclusive timing region (NTT.cu:2384-2428)
 //   -speedgpu 11  Nussbaumer product on the GPU in the reference's ring
 //                 Z/(2^32-1) (test_nussbaumer, NTT.cu:1987-2005; -speedcpu 6 there)
-//   -param ref|p-I|p-III   parameter set (reference: compile-time QTESLA set)
+//   -param ref|p-I|p-III|p-III-4096|p-III-8192   parameter set (reference:
+//                 compile-time QTESLA set; the n = 4096 / 8192 sets run every
+//                 option but 11, whose Nussbaumer split is n <= 2048)
 //   -batch B      polynomials per batch (reference: BATCH macro, main.cuh:7)
 //   -r seed       random operands from the device generator (reference parses
 //                 -r but never uses it, main.cu:89-91); default: all-ones
@@ -55,7 +57,7 @@
 
 static void help_message()
 {
-    printf("usage: ntt_main -speedgpu {4,6,7,8,9,10,11} [-param ref|p-I|p-III] [-batch B] [-reps R] [-r seed] [-pcie] [-debug]\n");
+    printf("usage: ntt_main -speedgpu {4,6,7,8,9,10,11} [-param ref|p-I|p-III|p-III-4096|p-III-8192] [-batch B] [-reps R] [-r seed] [-pcie] [-debug]\n");
 }
 
 struct Opts {
@@ -281,7 +283,8 @@ int main(int argc, char **argv)
         if (a == "-speedgpu") { o.option = atoi(next()); i += 2; }
         else if (a == "-param") {
             std::string p = next();
-            o.ps = p == "ref" ? NTT_PARAM_REF : p == "p-I" ? NTT_PARAM_P_I : p == "p-III" ? NTT_PARAM_P_III : -1;
+            o.ps = p == "ref" ? NTT_PARAM_REF : p == "p-I" ? NTT_PARAM_P_I : p == "p-III" ? NTT_PARAM_P_III
+                 : p == "p-III-4096" ? NTT_PARAM_N4096 : p == "p-III-8192" ? NTT_PARAM_N8192 : -1;
             i += 2;
         }
         else if (a == "-batch") { o.batch = strtoull(next(), nullptr, 10); i += 2; }

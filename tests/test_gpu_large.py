@@ -336,3 +336,21 @@ def test_large_expired_slot_barrier_writes_sentinel(ntt, dev, ps):
     assert L.ntt_sync_expiries(ctypes.byref(c)) == 0
     assert c.value > 0
     assert ntt.sync_expiries() == 0   # the product library's own counter is untouched
+
+
+@pytest.mark.parametrize("ps", LARGE_SETS)
+def test_large_host_driver_kat(ps):
+    """The C++ host driver (reference CLI) at n = 4096 / 8192: CT-GS
+    composition and fused product report the all-ones KAT as Identical, the
+    transform round trip and the host pipeline pass; Nussbaumer (option 11)
+    fails with the library's NTT_ERR_PARAM."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "ntt-gpu-qtesla_amd", "bin", "ntt_main")
+    for opt, batch in (("6", "4"), ("7", "4"), ("9", "300"), ("10", "1500")):
+        args = [exe, "-speedgpu", opt, "-param", ps, "-batch", batch] + (["-r", "5"] if opt == "9" else [])
+        r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "Identical." in r.stdout, r.stdout + r.stderr
+    r = subprocess.run([exe, "-speedgpu", "11", "-param", ps, "-batch", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
