@@ -374,6 +374,123 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
     fwd_pass1_tw<P>(r, h, tw_base<PS, false>(), sw);
 }
 
+// ---- typed forward for poly_mul (MUL_LAZYBIAS) ---------------------------
+// Inside the fused product the forward's outputs never leave the kernel, so a
+// butterfly may skip the +2q bias of y' = a - t + 2q when the value's next
+// consumer tolerates a signed value in (-2q, 2q) ("S" type; "U" = [0, 4q)):
+// a reduction (min(x, x + 2q) instead of min(x, x - 2q)), BaseMul's
+// canonicalisation, or a multiply by a signed Shoup product with a centred
+// twiddle.  That turns the v_add3 of y' into a v_add.  Which registers are S
+// is fixed at compile time by the stage structure (register j after pass-1
+// stage s <= 3 is S iff it was the y output).  Pass 1's S-typed multiplies
+// use the centred twiddles below (compile-time literals, k < 32); pass 2's
+// lane twiddles exist unsigned only, so there a y' is left S only when its
+// consumer is an x input or BaseMul.
+#ifndef MUL_LAZYBIAS
+#define MUL_LAZYBIAS 0   // measured neutral (p-III +1 %, p-I -1 %, profiles/r03/ab_polymul_zsplit_lz.log)
+#endif
+__host__ __device__ constexpr uint32_t cbrv32(uint32_t x, int bits)
+{
+    uint32_t r = 0;
+    for (int i = 0; i < bits; i++) r |= ((x >> i) & 1u) << (bits - 1 - i);
+    return r;
+}
+// (-ws mod 2^32, wps) of forward twiddle k < 32, ws = psi^brv(k) centred
+template <class P>
+struct FwdSignedTw {
+    uint32_t wn[32], wp[32];
+    constexpr FwdSignedTw() : wn(), wp()
+    {
+        for (uint32_t k = 0; k < 32; k++) {
+            const TwPair c = csigned_tw(cpow(P::PSI, cbrv32(k, P::LOGN), P::Q), P::Q);
+            wn[k] = 0u - c.x;
+            wp[k] = c.y;
+        }
+    }
+};
+
+// CT butterfly with typed operands: XS / YS = x / y in S form, YOS = leave
+// y' in S form (no +2q); RED = reduce x (off for canonical inputs).  y in S
+// form takes the signed Shoup quotient (centred twiddle (wsn, wps)).
+template <uint32_t Q, bool RED, bool XS, bool YS, bool YOS>
+__device__ __forceinline__ void ct_bfly_t(uint32_t &x, uint32_t &y, uint32_t wn, uint32_t wp)
+{
+    const uint32_t a = !RED ? x : XS ? umin(x, x + 2 * Q) : csub<2 * Q>(x);   // [0, 2q)
+    uint32_t qe;
+    if constexpr (YS) qe = (uint32_t)(((int64_t)(int32_t)y * (int32_t)wp - 0x80000000ll) >> 32);
+    else qe = __umulhi(y, wp);
+    const uint32_t tn = madlo32(qe, Q, y * wn);   // -t, t in [0, 2q)
+    x = a - tn;
+    y = YOS ? a + tn : a + tn + 2 * Q;
+}
+
+template <class P>
+__device__ __forceinline__ void fwd_pass1_lz(uint32_t (&r)[32], uint32_t h, const uint2 *tw, const uint2 *sw)
+{
+    constexpr FwdSignedTw<P> ST{};
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const int hh = 16 >> s;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const uint32_t k = (1u << s) + (uint32_t)(j >> (5 - s));
+                // both inputs were outputs of the same kind of the previous stage
+                const bool ts = s > 0 && (j & (2 * hh)) != 0;
+                if (s == 0) {
+                    const uint2 w = tw[k];
+                    ct_bfly_t<P::Q, false, false, false, true>(r[j], r[j + hh], w.x, w.y);   // canonical inputs
+                } else if (ts) {
+                    if (s < 4) ct_bfly_t<P::Q, true, true, true, true>(r[j], r[j + hh], ST.wn[k], ST.wp[k]);
+                    else ct_bfly_t<P::Q, true, true, true, false>(r[j], r[j + hh], ST.wn[k], ST.wp[k]);
+                } else {
+                    const uint2 w = tw[k];
+                    if (s < 4) ct_bfly_t<P::Q, true, false, false, true>(r[j], r[j + hh], w.x, w.y);
+                    else ct_bfly_t<P::Q, true, false, false, false>(r[j], r[j + hh], w.x, w.y);   // U into the swap / transpose
+                }
+            }
+        }
+    }
+    if constexpr (P::LOGN == 11) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
+            r[2 * m] = pr[0];
+            r[2 * m + 1] = pr[1];
+            const uint2 w = sw[2 * m + h];
+            ct_bfly<P::Q>(r[2 * m], r[2 * m + 1], w.x, w.y);
+        }
+    }
+}
+
+// pass 2 down to pos bit BMIN (U inputs from the transpose).  A y' stays S
+// when its consumer is an x input of the next stage or (last stage) BaseMul;
+// so after the last stage register j is S iff j & 2^BMIN.
+template <class P, int BMIN>
+__device__ __forceinline__ void fwd_pass2_lz(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
+{
+#pragma unroll
+    for (int b = 4; b >= BMIN; --b) {
+        const int hh = 1 << b;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if ((j & hh) == 0) {
+                const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
+                const uint2 w = tab[e * 64 + lane];
+                const bool xs = b < 4 && (j & (2 * hh)) != 0;          // x came out S from stage b+1
+                const bool yos = b == BMIN || ((j + hh) & (hh >> 1)) == 0;
+                if (xs) {
+                    if (yos) ct_bfly_t<P::Q, true, true, false, true>(r[j], r[j + hh], w.x, w.y);
+                    else ct_bfly_t<P::Q, true, true, false, false>(r[j], r[j + hh], w.x, w.y);
+                } else {
+                    if (yos) ct_bfly_t<P::Q, true, false, false, true>(r[j], r[j + hh], w.x, w.y);
+                    else ct_bfly_t<P::Q, true, false, false, false>(r[j], r[j + hh], w.x, w.y);
+                }
+            }
+        }
+    }
+}
+
 // BMIN > 0 stops short: the stages on pos bits BMIN-1..0 are left out
 // (poly_mul's incomplete transform, BaseMul)
 template <class P, int BMIN = 0>
@@ -422,6 +539,9 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
 // final scaling with (n/D)^-1); outputs above 2q get one conditional
 // subtraction.  Replaces LOGR stages of each forward and of the inverse and
 // the pointwise product.
+#ifndef MUL_ZSPLIT
+#define MUL_ZSPLIT 1
+#endif
 template <class P, int LOGR>
 struct BaseMul {
     static constexpr int D = 1 << LOGR;
@@ -432,20 +552,92 @@ struct BaseMul {
     static_assert(D * QD * QD / 4294967296.0 + QD < 4.0 * QD, "one conditional subtraction reaches [0, 2q)");
     static constexpr int E0 = (1 << (4 - LOGR)) - 1;   // LDS entry of the stage on pos bit LOGR
 
+    // zeta-split form (MUL_ZSPLIT): c_k = L_k + zeta R * REDC(H_k), L_k / H_k the
+    // sums of the D products without / with the wrap (a, b canonical, H_k
+    // < (D-1) q^2), zeta R = zeta 2^32 mod q in [0, q] per residue PAIR (the
+    // +w / -w residues share w).  Per residue that is 7 x (REDC + one 64-bit
+    // multiply-add) instead of 7 b~ products (Shoup + two-candidate min).
+    // Bound: c_k < (k+1) q^2 + q ((D-1-k) q^2 / 2^32 + q) <= (D + q/2^32) q^2.
+    static constexpr double CZ = (D + QD / 4294967296.0) * QD * QD;
+    static_assert(CZ + 4294967296.0 * QD < 18446744073709551616.0, "zeta-split REDC input fits 64 bits");
+    static_assert(CZ / 4294967296.0 + QD < 4.0 * QD, "zeta-split: one conditional subtraction reaches [0, 2q)");
+    static constexpr bool OUT_CSUB_Z = CZ / 4294967296.0 + QD >= 2.0 * QD;
+
+    static __device__ __forceinline__ uint32_t redc(uint64_t c)
+    {
+        const uint32_t m = (uint32_t)c * P::QNEG;
+        return (uint32_t)(((uint64_t)m * P::Q + c) >> 32);
+    }
+
+    // [0,4q) (U) or (-2q,2q) (S, MUL_LAZYBIAS) -> canonical [0,q)
+    // (s is a compile-time constant once the residue loop is unrolled)
+    static __device__ __forceinline__ uint32_t canon(bool s, uint32_t x)
+    {
+        return s ? csub<P::Q>(umin(x, x + P::Q2)) : canon4<P>(x);
+    }
+
+    // ODD_S: the odd residues (registers with bit LOGR set) hold S-form values
+    template <bool ODD_S>
+    static __device__ __forceinline__ void run_zsplit(uint32_t (&ra)[32], const uint32_t (&rb)[32], const uint2 *tab,
+                                                      uint32_t lane)
+    {
+#pragma unroll
+        for (int gp = 0; gp < 16 / D; ++gp) {
+            const uint2 w = tab[(E0 + gp) * 64 + lane];   // (-w mod 2^32, w')
+            // -(w R mod q) in (-2q, 0] (negated Shoup product of the constant R)
+            const uint32_t tn = madlo32(__umulhi(P::R, w.y), P::Q, P::R * w.x);
+            const uint32_t zr[2] = {umin(0u - tn, (0u - P::Q) - tn),   // +w: w R mod q in [0, q]
+                                    umin(tn + P::Q, tn + P::Q2)};      // -w
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int g = 2 * gp + e;
+                uint32_t z = zr[e];
+                asm volatile("" : "+v"(z));   // one residue at a time (no interleaving of the pair: it spills)
+                uint32_t a[D], b[D];
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+                    a[i] = canon(ODD_S && (g & 1), ra[D * g + i]);
+                    b[i] = canon(ODD_S && (g & 1), rb[D * g + i]);
+                }
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    uint64_t c = 0;
+#pragma unroll
+                    for (int i = 0; i <= k; ++i) c += (uint64_t)a[i] * b[k - i];
+                    if (k < D - 1) {
+                        uint64_t hs = 0;
+#pragma unroll
+                        for (int i = k + 1; i < D; ++i) hs += (uint64_t)a[i] * b[k + D - i];
+                        c += (uint64_t)z * redc(hs);
+                    }
+                    const uint32_t r = redc(c);
+                    ra[D * g + k] = OUT_CSUB_Z ? csub<P::Q2>(r) : r;
+                }
+            }
+        }
+    }
+
+    template <bool ODD_S = false>
     static __device__ __forceinline__ void run(uint32_t (&ra)[32], const uint32_t (&rb)[32], const uint2 *tab, uint32_t lane)
     {
+#if MUL_ZSPLIT
+        if constexpr (D >= 2) {
+            run_zsplit<ODD_S>(ra, rb, tab, lane);
+            return;
+        }
+#endif
 #pragma unroll
         for (int g = 0; g < 32 / D; ++g) {
             const uint2 w = tab[(E0 + (g >> 1)) * 64 + lane];   // (-w mod 2^32, w')
             uint32_t a[D], b[D], bt[D];
 #pragma unroll
             for (int i = 0; i < D; ++i) {
-                a[i] = canon4<P>(ra[D * g + i]);
-                b[i] = canon4<P>(rb[D * g + i]);
+                a[i] = canon(ODD_S && (g & 1), ra[D * g + i]);
+                b[i] = canon(ODD_S && (g & 1), rb[D * g + i]);
             }
 #pragma unroll
             for (int i = 1; i < D; ++i) {
-                const uint32_t y = rb[D * g + i];
+                const uint32_t y = b[i];
                 const uint32_t tn = madlo32(__umulhi(y, w.y), P::Q, y * w.x);   // -(b w mod q), in (-2q, 0]
                 // zeta b_i in [0, q]: +w -> min(-tn, -tn - q); -w -> min(tn + q, tn + 2q)
                 bt[i] = (g & 1) ? umin(tn + P::Q, tn + P::Q2) : umin(0u - tn, (0u - P::Q) - tn);
@@ -800,9 +992,12 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
                 if (valid) st_out(pc + LT::S * j, ra[j] + rb[j]);
             continue;
         }
-        fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+        constexpr bool LZ = !BHAT && MUL_LAZYBIAS;   // typed forwards (fwd_pass1_lz)
+        if constexpr (LZ) fwd_pass1_lz<P>(ra, L.h, tw_base<PS, false>(), ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+        else fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
         lds_p1_to_p2<P>(ra, buf, BHAT ? L : LT(opaque_lane()));
-        fwd_pass2<P, BHAT ? 0 : mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
+        if constexpr (LZ) fwd_pass2_lz<P, mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
+        else fwd_pass2<P, BHAT ? 0 : mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
         // b-hat is in natural order: register j of the pass-2 layout holds
         // index brv5(j)*S + lane (the forward's store mapping)
         if constexpr (VAR == 2) {
@@ -820,10 +1015,12 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
             // incomplete domain: both forwards stop above pos bit LOGR-1,
             // products mod x^(2^LOGR) -+ zeta, the inverse starts at pos bit
             // LOGR (BaseMul)
-            fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+            if constexpr (LZ) fwd_pass1_lz<P>(rb, L.h, tw_base<PS, false>(), ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+            else fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
             lds_p1_to_p2<P>(rb, buf, LT(opaque_lane()));
-            fwd_pass2<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
-            BaseMul<P, mul_logr<PS>()>::run(ra, rb, ftw2 + opaque_zero(), L.lane);
+            if constexpr (LZ) fwd_pass2_lz<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
+            else fwd_pass2<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
+            BaseMul<P, mul_logr<PS>()>::template run<LZ>(ra, rb, ftw2 + opaque_zero(), L.lane);
             inv_pass2<P, mul_logr<PS>()>(ra, itw2 + opaque_zero(), L.lane);
             lds_p2_to_p1<P>(ra, buf, LT(opaque_lane()));
             inv_pass1<PS, P, P::template ninv_r<mul_logr<PS>()>(), P::template c1_r<mul_logr<PS>()>()>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);

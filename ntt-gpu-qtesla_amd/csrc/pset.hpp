@@ -43,6 +43,7 @@ struct PSet {
     static constexpr int LOGN = LOGN_;
     static constexpr uint32_t N = 1u << LOGN_;
     static constexpr uint32_t Q2 = 2 * Q_;
+    static constexpr uint32_t PSI = PSI_;
     static constexpr uint32_t QNEG = cqinv_neg(Q_);
     static constexpr uint32_t NINV = cpow(N, Q_ - 2, Q_);
     static constexpr uint32_t PSI_INV = cpow(PSI_, Q_ - 2, Q_);

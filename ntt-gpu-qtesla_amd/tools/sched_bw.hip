@@ -118,13 +118,13 @@ __device__ __forceinline__ void unit_copy(uint32_t *buf, uint32_t u, uint32_t la
 }
 
 // ---- chunk: the library's schedule ---------------------------------------
-template <bool NT, int ITER>
-__global__ __launch_bounds__(512) void k_chunk(uint32_t *buf, uint32_t nunits, uint32_t ppw)
+template <bool NT, int ITER, int WPB = 8>
+__global__ __launch_bounds__(64 * WPB) void k_chunk(uint32_t *buf, uint32_t nunits, uint32_t ppw)
 {
     extern __shared__ uint32_t dyn[];
     const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t u = blockIdx.x * 8 * ppw + w;
-    for (uint32_t i = 0; i < ppw; ++i, u += 8) {
+    uint32_t u = blockIdx.x * WPB * ppw + w;
+    for (uint32_t i = 0; i < ppw; ++i, u += WPB) {
         if (u >= nunits) break;
         unit_copy<NT, ITER>(buf, u, lane);
     }
@@ -289,6 +289,14 @@ int main(int argc, char **argv)
         const uint32_t grid = (npoly + 8 * PPW - 1) / (8 * PPW);                                                 \
         hipLaunchKernelGGL((k_chunk<NT, ITER>), dim3(grid), dim3(512), LDS80, 0, a, npoly, (uint32_t)PPW);     \
     });
+// the chunk schedule at other occupancies: WPB waves per workgroup, LDSK KiB
+// pinned per workgroup (round 3, session 2: would smaller transpose buffers pay?)
+#define CHUNKX(NT, ITER, PPW, WPB, LDSK)                                                                         \
+    snprintf(nm, sizeof nm, "chunkx nt=%d iter=%d ppw=%d wpb=%d lds=%dK", NT, ITER, PPW, WPB, LDSK);            \
+    add(nm, [=] {                                                                                                \
+        const uint32_t grid = (npoly + WPB * PPW - 1) / (WPB * PPW);                                             \
+        hipLaunchKernelGGL((k_chunk<NT, ITER, WPB>), dim3(grid), dim3(64 * WPB), (LDSK) * 1024, 0, a, npoly, (uint32_t)PPW); \
+    });
 #define STRIDE(NT, ITER)                                                                                         \
     snprintf(nm, sizeof nm, "stride nt=%d iter=%d lds=80K", NT, ITER);                                          \
     add(nm, [=] { hipLaunchKernelGGL((k_stride<NT, ITER>), dim3(2 * cus), dim3(512), LDS80, 0, a, npoly); });
@@ -308,10 +316,28 @@ int main(int argc, char **argv)
         CK(hipMemsetAsync(ctr, 0, 8 * 128, 0));                                                                  \
         hipLaunchKernelGGL((k_sync_stride<NT, ITER, K>), dim3(2 * cus), dim3(512), LDS80, 0, a, npoly, ctr);    \
     });
+    if (getenv("SCHED_OCC")) {
+        CHUNKX(true, 0, 16, 8, 80)
+        CHUNKX(true, 0, 4, 8, 80)
+        CHUNKX(true, 0, 16, 8, 48)
+        CHUNKX(true, 0, 4, 8, 48)
+        CHUNKX(true, 0, 16, 10, 56)
+        CHUNKX(true, 0, 4, 10, 56)
+        CHUNKX(true, 0, 16, 8, 40)
+        CHUNKX(true, 0, 4, 8, 40)
+        CHUNKX(true, 0, 16, 4, 32)
+        CHUNKX(true, 20, 16, 8, 80)
+        CHUNKX(true, 20, 16, 8, 48)
+        CHUNKX(true, 20, 16, 10, 56)
+        CHUNKX(true, 40, 16, 8, 80)
+        CHUNKX(true, 40, 16, 8, 48)
+        CHUNKX(true, 40, 16, 10, 56)
+    } else {
     SSTR(true, 0, 1)
     SSTR(true, 0, 2)
     SSTR(true, 0, 4)
     SSTR(true, 0, 16)
+    }
     CHUNK(true, 0, 16)
     CHUNK(true, 0, 4)
     STRIDE(true, 0)
