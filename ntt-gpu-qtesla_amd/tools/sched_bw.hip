@@ -131,6 +131,36 @@ __global__ __launch_bounds__(64 * WPB) void k_chunk(uint32_t *buf, uint32_t nuni
     if (nunits == 0) dyn[threadIdx.x] = 0;
 }
 
+// chunk schedule, software-pipelined: unit i+1's loads are issued before unit
+// i's stores (one vmcnt counts both on gfx9-family, so in the plain loop the
+// first wait for unit i+1's data also waits for unit i's store acks)
+template <bool NT, int ITER>
+__global__ __launch_bounds__(512) void k_chunk_pipe(uint32_t *buf, uint32_t nunits, uint32_t ppw)
+{
+    extern __shared__ uint32_t dyn[];
+    const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t u = blockIdx.x * 8 * ppw + w;
+    if (u >= nunits) return;
+    uint32_t cur[32], nxt[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) cur[j] = ld<NT>(buf + (size_t)u * NWORDS_POLY + lane + 64 * j);
+    for (uint32_t i = 0; i < ppw; ++i, u += 8) {
+        const bool more = i + 1 < ppw && u + 8 < nunits;
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) nxt[j] = ld<NT>(buf + (size_t)(u + 8) * NWORDS_POLY + lane + 64 * j);
+        }
+        work32<ITER>(cur);
+        uint32_t *p = buf + (size_t)u * NWORDS_POLY + lane;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) st<NT>(p + 64 * j, cur[j]);
+        if (!more) break;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) cur[j] = nxt[j];
+    }
+    if (nunits == 0) dyn[threadIdx.x] = 0;
+}
+
 // ---- grid-stride persistent -----------------------------------------------
 template <bool NT, int ITER>
 __global__ __launch_bounds__(512) void k_stride(uint32_t *buf, uint32_t nunits)
@@ -316,6 +346,20 @@ int main(int argc, char **argv)
         CK(hipMemsetAsync(ctr, 0, 8 * 128, 0));                                                                  \
         hipLaunchKernelGGL((k_sync_stride<NT, ITER, K>), dim3(2 * cus), dim3(512), LDS80, 0, a, npoly, ctr);    \
     });
+#define CHUNKP(NT, ITER, PPW)                                                                                    \
+    snprintf(nm, sizeof nm, "chunk-pipe nt=%d iter=%d ppw=%d lds=80K", NT, ITER, PPW);                          \
+    add(nm, [=] {                                                                                                \
+        const uint32_t grid = (npoly + 8 * PPW - 1) / (8 * PPW);                                                 \
+        hipLaunchKernelGGL((k_chunk_pipe<NT, ITER>), dim3(grid), dim3(512), LDS80, 0, a, npoly, (uint32_t)PPW); \
+    });
+    if (getenv("SCHED_PIPE")) {
+        CHUNKP(true, 0, 16)
+        CHUNKP(true, 0, 4)
+        CHUNKP(true, 20, 16)
+        CHUNKP(true, 40, 16)
+        CHUNK(true, 20, 16)
+        CHUNK(true, 40, 16)
+    }
     if (getenv("SCHED_OCC")) {
         CHUNKX(true, 0, 16, 8, 80)
         CHUNKX(true, 0, 4, 8, 80)
