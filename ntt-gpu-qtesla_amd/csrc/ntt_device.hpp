@@ -387,7 +387,7 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
 // lane twiddles exist unsigned only, so there a y' is left S only when its
 // consumer is an x input or BaseMul.
 #ifndef MUL_LAZYBIAS
-#define MUL_LAZYBIAS 0   // measured neutral (p-III +1 %, p-I -1 %, profiles/r03/ab_polymul_zsplit_lz.log)
+#define MUL_LAZYBIAS 1   // with MUL_HOIST: -1.4 % (p-III) / -2.2 % (p-I); alone +1.5 % / +0.9 % (profiles/r03/ab_polymul_*.log)
 #endif
 __host__ __device__ constexpr uint32_t cbrv32(uint32_t x, int bits)
 {
@@ -539,6 +539,13 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
 // final scaling with (n/D)^-1); outputs above 2q get one conditional
 // subtraction.  Replaces LOGR stages of each forward and of the inverse and
 // the pointwise product.
+#ifndef MUL_HOIST
+// poly_mul's transposes with loop-invariant lane addresses instead of the
+// per-transpose recomputation from an opaque lane (which kept the r02 kernel
+// from spilling): affordable once MUL_LAZYBIAS took the p-III kernel from 126
+// to 96 VGPRs (121 with the hoisted addresses, no spills)
+#define MUL_HOIST 1
+#endif
 #ifndef MUL_ZSPLIT
 #define MUL_ZSPLIT 1
 #endif
@@ -995,7 +1002,7 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
         constexpr bool LZ = !BHAT && MUL_LAZYBIAS;   // typed forwards (fwd_pass1_lz)
         if constexpr (LZ) fwd_pass1_lz<P>(ra, L.h, tw_base<PS, false>(), ftw2 + TW2_ENTRIES * 64 + opaque_zero());
         else fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
-        lds_p1_to_p2<P>(ra, buf, BHAT ? L : LT(opaque_lane()));
+        lds_p1_to_p2<P>(ra, buf, (BHAT || MUL_HOIST) ? L : LT(opaque_lane()));
         if constexpr (LZ) fwd_pass2_lz<P, mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
         else fwd_pass2<P, BHAT ? 0 : mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
         // b-hat is in natural order: register j of the pass-2 layout holds
@@ -1017,12 +1024,12 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
             // LOGR (BaseMul)
             if constexpr (LZ) fwd_pass1_lz<P>(rb, L.h, tw_base<PS, false>(), ftw2 + TW2_ENTRIES * 64 + opaque_zero());
             else fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
-            lds_p1_to_p2<P>(rb, buf, LT(opaque_lane()));
+            lds_p1_to_p2<P>(rb, buf, MUL_HOIST ? L : LT(opaque_lane()));
             if constexpr (LZ) fwd_pass2_lz<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
             else fwd_pass2<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
             BaseMul<P, mul_logr<PS>()>::template run<LZ>(ra, rb, ftw2 + opaque_zero(), L.lane);
             inv_pass2<P, mul_logr<PS>()>(ra, itw2 + opaque_zero(), L.lane);
-            lds_p2_to_p1<P>(ra, buf, LT(opaque_lane()));
+            lds_p2_to_p1<P>(ra, buf, MUL_HOIST ? L : LT(opaque_lane()));
             inv_pass1<PS, P, P::template ninv_r<mul_logr<PS>()>(), P::template c1_r<mul_logr<PS>()>()>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
         } else {
 #pragma unroll
