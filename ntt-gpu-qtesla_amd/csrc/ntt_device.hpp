@@ -539,6 +539,9 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
 // final scaling with (n/D)^-1); outputs above 2q get one conditional
 // subtraction.  Replaces LOGR stages of each forward and of the inverse and
 // the pointwise product.
+#ifndef NTT_FWD_LZ
+#define NTT_FWD_LZ 0   // A/B switch: poly_ntt with the typed lazy-bias passes (HBM-bound: -0.6 % p-III, 0 p-I, profiles/r03/ab_fwd_lazybias.log)
+#endif
 #ifndef MUL_HOIST
 // poly_mul's transposes with loop-invariant lane addresses instead of the
 // per-transpose recomputation from an opaque lane (which kept the r02 kernel
@@ -839,17 +842,24 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     };
     // canonical output: BR=false from the bit-reversed pass-2 registers to
     // natural order, brv5(j)*S + lane; BR=true from the pass-1 arrangement
+    // NTT_FWD_LZ: the typed lazy-bias passes of poly_mul (fwd_pass1_lz /
+    // fwd_pass2_lz down to bit 0: odd registers end in S form)
+    constexpr bool LZ = NTT_FWD_LZ && !BR;
     auto store = [&](uint32_t (&r)[32], uint32_t u) {
         const uint32_t poly = L.poly(u);
         if (LT::BIG || poly < npoly) {
             uint32_t *dst = out + LT::unit_base(u) + L.col();
             if constexpr (BR) dst += LT::BIG ? 32 * L.h : 0u;   // brl + 32 h = l5 + 64 h (p1s_off)
 #pragma unroll
-            for (int j = 0; j < 32; ++j) st_out(dst + (BR ? p1s_off<P>(j) : brv5(j) * LT::S), canon4<P>(r[j]));
+            for (int j = 0; j < 32; ++j) {
+                const uint32_t v = (LZ && (j & 1)) ? csub<P::Q>(umin(r[j], r[j] + P::Q2)) : canon4<P>(r[j]);
+                st_out(dst + (BR ? p1s_off<P>(j) : brv5(j) * LT::S), v);
+            }
         }
     };
     auto front = [&](uint32_t (&r)[32], uint32_t) {
-        fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        if constexpr (LZ) fwd_pass1_lz<P>(r, L.h, tw_base<PS, false>(), tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        else fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
         lds_p1_to_p2<P>(r, buf, L);
         if constexpr (BR) {
             fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
@@ -857,7 +867,8 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
         }
     };
     auto back = [&](uint32_t (&r)[32], uint32_t u) {
-        if constexpr (!BR) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        if constexpr (LZ) fwd_pass2_lz<P, 0>(r, tw2 + opaque_zero(), L.lane);
+        else if constexpr (!BR) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
         store(r, u);
     };
     auto process = [&](uint32_t (&r)[32], uint32_t u) {
