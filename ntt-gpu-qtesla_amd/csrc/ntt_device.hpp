@@ -510,7 +510,10 @@ __device__ __forceinline__ void fwd_pass2(uint32_t (&r)[32], const uint2 *tab, u
     }
 }
 
-template <class P, int BMIN = 0>
+// WIDE0: the first stage's inputs lie in [0, 3q) with |x - y| < 2^31
+// (poly_mul's BaseMul with a half-canonical first operand, MUL_AHALF, p-III:
+// [0, 2.19q)): x' = (x + y) mod 2q by a three-candidate min (v_min3)
+template <class P, int BMIN = 0, bool WIDE0 = false>
 __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
 {
 #pragma unroll
@@ -521,7 +524,13 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
             if ((j & hh) == 0) {
                 const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
                 const uint2 w = tab[e * 64 + lane];
-                gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+                if (WIDE0 && b == BMIN) {
+                    const uint32_t x = r[j], y = r[j + hh], sm = x + y;   // [0, 6q)
+                    r[j] = umin(umin(sm, sm - P::Q2), sm - 2 * P::Q2);
+                    r[j + hh] = sshoup_mul<P::Q>(x - y, w.x, w.y);
+                } else {
+                    gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+                }
             }
         }
     }
@@ -552,6 +561,9 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
 #ifndef MUL_ZSPLIT
 #define MUL_ZSPLIT 1
 #endif
+#ifndef MUL_AHALF
+#define MUL_AHALF 1   // p-III poly_mul -1.3 % (profiles/r03/ab_polymul_ahalf.log)
+#endif
 template <class P, int LOGR>
 struct BaseMul {
     static constexpr int D = 1 << LOGR;
@@ -572,6 +584,22 @@ struct BaseMul {
     static_assert(CZ + 4294967296.0 * QD < 18446744073709551616.0, "zeta-split REDC input fits 64 bits");
     static_assert(CZ / 4294967296.0 + QD < 4.0 * QD, "zeta-split: one conditional subtraction reaches [0, 2q)");
     static constexpr bool OUT_CSUB_Z = CZ / 4294967296.0 + QD >= 2.0 * QD;
+    // MUL_AHALF: a only reduced to [0, 2q) (one conditional subtraction
+    // instead of two), b canonical: c_k < 2 D q^2 (the k = D-1 sum; the others
+    // stay below (2D - 1 + 2q/2^32) q^2).  The REDC output may then pass 4q
+    // (p-III: 4.19q): one conditional subtraction leaves it below WH = 2.19q and
+    // the inverse's first stage takes such inputs (inv_pass2 WIDE0).
+    static constexpr double CZH = 2.0 * D * QD * QD;
+    static_assert(CZH + 4294967296.0 * QD < 18446744073709551616.0, "half-canonical REDC input fits 64 bits");
+    static constexpr double OUTH = CZH / 4294967296.0 + QD;
+    static constexpr double WH = OUTH >= 2.0 * QD ? OUTH - 2.0 * QD : OUTH;   // after the csub
+    static_assert(!(MUL_AHALF && OUT_CSUB_Z) || (WH < 3.0 * QD && WH < 2147483648.0 && 2.0 * WH < 4294967296.0),
+                  "first inverse stage: x + y < 6q fits 32 bits, |x - y| < 2^31");
+    static constexpr bool OUT_CSUB_H = OUTH >= 2.0 * QD;
+    // only where the z-split output already needs its conditional subtraction
+    // (p-III); elsewhere the half-canonical a would move one csub to the output
+    static constexpr bool AH = MUL_AHALF && OUT_CSUB_Z;
+    static constexpr bool WIDE = AH && OUTH >= 4.0 * QD;   // inverse's first stage in WIDE0 form
 
     static __device__ __forceinline__ uint32_t redc(uint64_t c)
     {
@@ -584,6 +612,11 @@ struct BaseMul {
     static __device__ __forceinline__ uint32_t canon(bool s, uint32_t x)
     {
         return s ? csub<P::Q>(umin(x, x + P::Q2)) : canon4<P>(x);
+    }
+    // the same to [0, 2q) only
+    static __device__ __forceinline__ uint32_t half(bool s, uint32_t x)
+    {
+        return s ? umin(x, x + P::Q2) : csub<P::Q2>(x);
     }
 
     // ODD_S: the odd residues (registers with bit LOGR set) hold S-form values
@@ -606,7 +639,7 @@ struct BaseMul {
                 uint32_t a[D], b[D];
 #pragma unroll
                 for (int i = 0; i < D; ++i) {
-                    a[i] = canon(ODD_S && (g & 1), ra[D * g + i]);
+                    a[i] = AH ? half(ODD_S && (g & 1), ra[D * g + i]) : canon(ODD_S && (g & 1), ra[D * g + i]);
                     b[i] = canon(ODD_S && (g & 1), rb[D * g + i]);
                 }
 #pragma unroll
@@ -621,7 +654,7 @@ struct BaseMul {
                         c += (uint64_t)z * redc(hs);
                     }
                     const uint32_t r = redc(c);
-                    ra[D * g + k] = OUT_CSUB_Z ? csub<P::Q2>(r) : r;
+                    ra[D * g + k] = (AH ? OUT_CSUB_H : OUT_CSUB_Z) ? csub<P::Q2>(r) : r;
                 }
             }
         }
@@ -1039,7 +1072,7 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
             if constexpr (LZ) fwd_pass2_lz<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
             else fwd_pass2<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
             BaseMul<P, mul_logr<PS>()>::template run<LZ>(ra, rb, ftw2 + opaque_zero(), L.lane);
-            inv_pass2<P, mul_logr<PS>()>(ra, itw2 + opaque_zero(), L.lane);
+            inv_pass2<P, mul_logr<PS>(), BaseMul<P, mul_logr<PS>()>::WIDE>(ra, itw2 + opaque_zero(), L.lane);
             lds_p2_to_p1<P>(ra, buf, MUL_HOIST ? L : LT(opaque_lane()));
             inv_pass1<PS, P, P::template ninv_r<mul_logr<PS>()>(), P::template c1_r<mul_logr<PS>()>()>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
         } else {

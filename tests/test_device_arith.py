@@ -200,3 +200,41 @@ def test_zeta_split_residue_product(name):
                 assert 0 <= r < 2 * q
                 want = (L + z * sum(a[i] * b[k + 8 - i] for i in range(k + 1, 8))) * rinv % q
                 assert r % q == want
+
+
+@pytest.mark.parametrize("name", list(PRIMES))
+def test_half_canonical_residue_product_and_wide_first_stage(name):
+    """MUL_AHALF (p-III, where the z-split output needs its csub anyway):
+    a in [0, 2q), b canonical -> c_k < 16 q^2 fits 64 bits with the REDC's
+    m q; the REDC output after one csub lies below 2.19 q (p-III), and the
+    inverse's first GS stage (inv_pass2 WIDE0) maps such x, y to
+    (x + y) mod 2q by a three-candidate min, with |x - y| < 2^31"""
+    q = PRIMES[name]
+    qneg = (-pow(q, -1, 1 << 32)) & M32
+    R = (1 << 32) % q
+    rinv = pow(R, -1, q)
+    rng = random.Random(5)
+    cases = [([2 * q - 1] * 8, [q - 1] * 8, q - 1)] + \
+        [([rng.randrange(2 * q) for _ in range(8)], [rng.randrange(q) for _ in range(8)], rng.randrange(q))
+         for _ in range(300)]
+    outs = []
+    for a, b, z in cases:
+        zr = z * R % q
+        for k in range(8):
+            L = sum(a[i] * b[k - i] for i in range(k + 1))
+            H = sum(a[i] * b[k + 8 - i] for i in range(k + 1, 8))
+            c = L + (zr * redc(H, q, qneg) if k < 7 else 0)
+            assert c < 16 * q * q and c + M32 * q <= M64
+            r = redc(c, q, qneg)
+            assert r < 16 * q * q / 2 ** 32 + q
+            r = min(r, (r - 2 * q) & M32)
+            assert (r - (L + z * H) * rinv) % q == 0
+            outs.append(r)
+    wh = max(16 * q * q / 2 ** 32 + q - 2 * q, 2 * q)
+    assert max(outs) < wh and wh < 3 * q and wh < 2 ** 31
+    for _ in range(2000):
+        x, y = rng.choice(outs), rng.choice(outs)
+        sm = (x + y) & M32
+        xo = min(sm, (sm - 2 * q) & M32, (sm - 4 * q) & M32)
+        assert xo == (x + y) % (2 * q)
+        assert abs(x - y) < 2 ** 31
