@@ -214,6 +214,84 @@ __device__ __forceinline__ void cross_gs(uint32_t (&r)[32], uint32_t *mine, cons
     ss.wait<G>();
 }
 
+// ---- in-register head (LARGE_HEAD) -----------------------------------------
+// The standalone transforms can run the g = log2 G stages on pos bits L-1 ..
+// 11 in registers instead of across waves: wave B loads chunk c's words
+// 2048 c + (2048/G) B + p (p < 2048/G) at register (32/G) c + j'
+// (p = 64 j' + l: G runs of 8/G KiB), so every radix-G group of a lane is
+// registers j', 32/G + j', ...; the head's butterflies and twiddles are the
+// cross stages' (c_cross).  One exchange then gives wave B its sub-block
+// (register (32/G) B' + j' = sub-block word (2048/G) B' + 64 j' + l, the
+// pass-1 layout): only the other waves' chunks move, (G-1)/G of the 32
+// words, one LDS round trip and two slot barriers in place of the cross
+// stages' g round trips of all 32 words and 2g barriers.
+#ifndef LARGE_HEAD
+#define LARGE_HEAD 1
+#endif
+#ifndef LARGE_HEAD_SKIPOWN
+#define LARGE_HEAD_SKIPOWN 1   // own chunk stays in registers (else it round-trips too)
+#endif
+template <class P, int G>
+__device__ __forceinline__ void head_fwd(uint32_t (&r)[32], const uint2 *cross)
+{
+    const uint2 w1 = cross[1];
+    if constexpr (G == 2) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) ct_bfly<P::Q, false>(r[j], r[16 + j], w1.x, w1.y);   // pos bit 11, inputs < 2q
+    } else {
+        const uint2 w2 = cross[2], w3 = cross[3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {   // pos bit 12 (k = 1): chunks c, c + 2; inputs < 2q
+            ct_bfly<P::Q, false>(r[j], r[16 + j], w1.x, w1.y);
+            ct_bfly<P::Q, false>(r[8 + j], r[24 + j], w1.x, w1.y);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {   // pos bit 11 (k = 2, 3): chunks c, c + 1
+            ct_bfly<P::Q>(r[j], r[8 + j], w2.x, w2.y);
+            ct_bfly<P::Q>(r[16 + j], r[24 + j], w3.x, w3.y);
+        }
+    }
+}
+template <class P, int G>
+__device__ __forceinline__ void head_inv(uint32_t (&r)[32], const uint2 *cross)
+{
+    const uint2 w1 = cross[1];
+    if constexpr (G == 4) {
+        const uint2 w2 = cross[2], w3 = cross[3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {   // pos bit 11 (k = 2, 3)
+            gs_bfly<P::Q>(r[j], r[8 + j], w2.x, w2.y);
+            gs_bfly<P::Q>(r[16 + j], r[24 + j], w3.x, w3.y);
+        }
+    }
+    constexpr int H = 16;   // pos bit L-1 (k = 1): chunks c, c + G/2
+#pragma unroll
+    for (int j = 0; j < H; ++j) gs_bfly<P::Q>(r[j], r[H + j], w1.x, w1.y);
+}
+// chunk c of wave B <-> chunk B of wave c among the slot's G waves (buffers
+// [j][lane], conflict-free; chunk B stays in registers); the second wait frees
+// the buffers for the next transpose / exchange
+template <int G>
+__device__ __forceinline__ void head_exchange(uint32_t (&r)[32], uint32_t *mine, const uint32_t *slot_bufs, uint32_t lane,
+                                              uint32_t B, SlotSync &ss)
+{
+    constexpr int C = 32 / G;
+#pragma unroll
+    for (int c = 0; c < G; ++c)
+        if (!LARGE_HEAD_SKIPOWN || (uint32_t)c != B)
+#pragma unroll
+            for (int j = 0; j < C; ++j) mine[(C * c + j) * 64 + lane] = r[C * c + j];
+    ss.wait<G>();
+#pragma unroll
+    for (int c = 0; c < G; ++c)
+        if (!LARGE_HEAD_SKIPOWN || (uint32_t)c != B) {
+            const uint32_t *src = slot_bufs + c * XPOSE_WORDS + B * C * 64 + lane;
+#pragma unroll
+            for (int j = 0; j < C; ++j) r[C * c + j] = src[j * 64];
+        }
+    ss.wait<G>();
+}
+
 // Position of sub-block output k' in its wave's 8 KiB exchange buffer: the
 // rotation by B 32/G words makes both sides conflict-free (ds_*_b32 runs as
 // two 32-lane groups, bank = dword mod 32) -- the owner accesses consecutive
@@ -297,13 +375,20 @@ struct LargeWave {
     // < 2q at register j of lane l = p' 64 j + brl) down to the pass-2
     // layout: register j of lane l holds sub-block output k' = brv5(j) 64 + l
     // of global index G k' + brv_g(B), in [0,4q)
+    // (LARGE_HEAD: the input is in the head's chunked layout instead, see
+    // head_fwd, and the first g stages run in registers + one exchange)
     __device__ __forceinline__ void fwd(uint32_t (&r)[32])
     {
         constexpr int G = LG::G;
-        constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1), then for n = 8192 pos bit 11 (k = 2 + B/2)
-        cross_ct<P, false, G>(r, buf, partner(D0), opaque_lane(), (B & D0) != 0, c_cross[LG::IDX][0][1], ss);
-        if constexpr (G == 4)
-            cross_ct<P, true, G>(r, buf, partner(1u), opaque_lane(), (B & 1u) != 0, c_cross[LG::IDX][0][2 + (B >> 1)], ss);
+        if constexpr (LARGE_HEAD) {
+            head_fwd<P, G>(r, c_cross[LG::IDX][0]);
+            head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, opaque_lane(), B, ss);
+        } else {
+            constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1), then for n = 8192 pos bit 11 (k = 2 + B/2)
+            cross_ct<P, false, G>(r, buf, partner(D0), opaque_lane(), (B & D0) != 0, c_cross[LG::IDX][0][1], ss);
+            if constexpr (G == 4)
+                cross_ct<P, true, G>(r, buf, partner(1u), opaque_lane(), (B & 1u) != 0, c_cross[LG::IDX][0][2 + (B >> 1)], ss);
+        }
         fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), bit5[0] + opaque_zero());
         lds_p1_to_p2<P>(r, buf, LT(opaque_lane()));   // addresses recomputed (see inv)
         subtree_scale<P, LG, false>(r, B);             // T_B = c_{B,b} T_0 (c_fscale)
@@ -362,10 +447,15 @@ struct LargeWave {
         inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5[1] + opaque_zero());
         const uint2 last = c_lastinv[LG::IDX][RS ? 1 : 0][B];
         inv_last_stage<P, false>(r, NINV, NINVP, last.x, last.y);   // [0,2q)
-        if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)
-            cross_gs<P, G>(r, buf, partner(1u), opaque_lane(), (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)], ss);
-        constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1)
-        cross_gs<P, G>(r, buf, partner(D0), opaque_lane(), (B & D0) != 0, c_cross[LG::IDX][1][1], ss);
+        if constexpr (LARGE_HEAD) {   // output in the head's chunked layout
+            head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, opaque_lane(), B, ss);
+            head_inv<P, G>(r, c_cross[LG::IDX][1]);
+        } else {
+            if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)
+                cross_gs<P, G>(r, buf, partner(1u), opaque_lane(), (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)], ss);
+            constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1)
+            cross_gs<P, G>(r, buf, partner(D0), opaque_lane(), (B & D0) != 0, c_cross[LG::IDX][1][1], ss);
+        }
     }
 };
 
@@ -385,8 +475,22 @@ __device__ __forceinline__ void large_steps(const LargeWave<LG> &w, uint32_t fir
     for (uint32_t it = 0; it < steps; ++it) {
         const uint32_t poly = first + it * LG::SLOTS + w.slot;
         const bool valid = poly < npoly;
-        step((size_t)(valid ? poly : first) * LG::PL::N + w.B * 2048u, valid);
+        step((size_t)(valid ? poly : first) * LG::PL::N, valid);
     }
+}
+
+// Word offset of register j from a wave's first word: the contiguous
+// sub-block layout (64 j), or with LARGE_HEAD the head's chunks (chunk c =
+// j / (32/G) at 2048 c); the wave's first word is 2048 B resp. (2048/G) B.
+template <class LG>
+__host__ __device__ constexpr uint32_t large_off(int j)
+{
+    return LARGE_HEAD ? 2048u * (uint32_t)(j / (32 / LG::G)) + 64u * (uint32_t)(j % (32 / LG::G)) : 64u * (uint32_t)j;
+}
+template <class LG>
+__device__ __forceinline__ uint32_t large_first(uint32_t B)
+{
+    return LARGE_HEAD ? B * (2048u / LG::G) : B * 2048u;
 }
 
 // the step's stores: a poisoned workgroup (expired slot barrier) writes sentinels
@@ -395,7 +499,7 @@ __device__ __forceinline__ void large_store(uint32_t *dst, const LargeWave<LG> &
 {
     const bool bad = w.ss.poisoned();
 #pragma unroll
-    for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, bad ? SYNC_SENTINEL : val(j));
+    for (int j = 0; j < 32; ++j) st_out(dst + large_off<LG>(j), bad ? SYNC_SENTINEL : val(j));
 }
 
 // The standalone transforms keep their own step bodies (the same dataflow as
@@ -411,6 +515,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
     using LT = Lane<P>;
     constexpr int G = LG::G;
     constexpr uint32_t N = LG::PL::N;
+    constexpr bool HEAD = LARGE_HEAD;
     __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
     const uint32_t first = blockIdx.x * (LG::SLOTS * ppw);
     if (first >= npoly) return;   // whole workgroup
@@ -436,6 +541,15 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
         uint32_t lo = L.brl;
         asm volatile("" : "+v"(lo));
         uint32_t r[32];
+        if constexpr (HEAD) {
+            // in-register head (LARGE_HEAD): chunk c's words 2048 c +
+            // (2048/G) B + 64 j' + l at register (32/G) c + j', the first g
+            // stages in registers, one exchange
+            load32(r, in + (size_t)(valid ? poly : first) * N + B * (2048u / G) + lo,
+                   [](int j) { return 2048 * (j / (32 / G)) + 64 * (j % (32 / G)); });
+            head_fwd<P, G>(r, c_cross[LG::IDX][0]);
+            head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, L.lane, B, ss);
+        } else {
         load32(r, in + (size_t)(valid ? poly : first) * N + B * 2048u + lo, [](int j) { return 64 * j; });
         // pos bit L-1 (k = 1), then for n = 8192 pos bit 11 (k = 2 + B/2)
         constexpr uint32_t D0 = G / 2;
@@ -443,6 +557,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large
         if constexpr (G == 4)
             cross_ct<P, true, G>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0,
                                  c_cross[LG::IDX][0][2 + (B >> 1)], ss);
+        }
         fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), bit5 + opaque_zero());
         lds_p1_to_p2<P>(r, buf, LT(opaque_lane()));   // addresses recomputed (see k_ntt_inv_large)
         subtree_scale<P, LG, false>(r, B);             // T_B = c_{B,b} T_0 (c_fscale)
@@ -480,6 +595,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
     constexpr int G = LG::G;
     constexpr uint32_t N = LG::PL::N;
     constexpr uint32_t NINVP = cshoup(LG::PL::NINV, P::Q);
+    constexpr bool HEAD = LARGE_HEAD;
     __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
     const uint32_t first = blockIdx.x * (LG::SLOTS * ppw);
     if (first >= npoly) return;
@@ -526,6 +642,19 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
         inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5 + opaque_zero());
         const uint2 last = c_lastinv[LG::IDX][0][B];
         inv_last_stage<P, false>(r, LG::PL::NINV, NINVP, last.x, last.y);   // [0,2q), scaled by n^-1
+        if constexpr (HEAD) {
+            // mirror of the forward's head: one exchange, the last g GS
+            // stages in registers, G runs stored
+            head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, L.lane, B, ss);
+            head_inv<P, G>(r, c_cross[LG::IDX][1]);
+            if (valid) {
+                const bool bad = ss.poisoned();
+                uint32_t *dst = out + (size_t)poly * N + B * (2048u / G) + lo;
+#pragma unroll
+                for (int j = 0; j < 32; ++j)
+                    st_out(dst + 2048 * (j / (32 / G)) + 64 * (j % (32 / G)), bad ? SYNC_SENTINEL : csub<P::Q>(r[j]));
+            }
+        } else {
         if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)
             cross_gs<P, G>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)], ss);
         constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1)
@@ -535,6 +664,7 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
             uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
 #pragma unroll
             for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, bad ? SYNC_SENTINEL : csub<P::Q>(r[j]));
+        }
         }
     }
 }
@@ -572,15 +702,19 @@ void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_
     if (first >= npoly) return;
     LargeWave<LG> w;
     w.template init<0, 1>(lds);
-    auto step = [&](size_t base, bool valid) {
+    auto step = [&](size_t pbase, bool valid) {
         uint32_t ra[32], rb[32];
+        // this wave's words: the forward's input layout (large_off), b-hat
+        // contiguous (the scatter of from_contiguous)
+        const size_t base = pbase + large_first<LG>(w.B), bbase = BHAT ? pbase + w.B * 2048u : base;
+        auto boff = [](int j) { return BHAT ? 64u * (uint32_t)j : large_off<LG>(j); };
         // both operands' loads issued up front: b's latency hides behind a's
         // transform (its 32 words are live there either way, as a's are
         // through b's transform)
-        load32(ra, a + base + opaque_lane(), [](int j) { return 64 * j; });
-        if (PF) load32(rb, b + base + opaque_lane(), [](int j) { return 64 * j; });
+        load32(ra, a + base + opaque_lane(), [](int j) { return large_off<LG>(j); });
+        if (PF) load32(rb, b + bbase + opaque_lane(), boff);
         w.fwd(ra);
-        if (!PF) load32(rb, b + base + opaque_lane(), [](int j) { return 64 * j; });
+        if (!PF) load32(rb, b + bbase + opaque_lane(), boff);
         if constexpr (BHAT) {   // b-hat < 2q
             // the scatter writes the partners' buffers: their forward
             // transposes (lds_p1_to_p2 on their own buffers) must be done
