@@ -681,9 +681,11 @@ __global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large
 // and b, one write of c.  a, b and c may alias: the G waves of a slot load
 // all of a and b before the slot barriers that precede any store.
 #ifndef MUL_LARGE_WAVES
-#define MUL_LARGE_WAVES 8   // n = 8192 product with both operands transformed: 8 waves at 2 per
-                             // SIMD (199 VGPRs) 6.68 ms vs 12 at 3 (37 VGPRs spilled) 6.77 ms per
-                             // 2^17 products (profiles/r03/ab_mul_large.log)
+#define MUL_LARGE_WAVES 12   // n = 8192 product with both operands transformed: with the cross-wave
+                              // stages 8 waves at 2 per SIMD (199 VGPRs) beat 12 at 3 (37 VGPRs
+                              // spilled), 6.68 vs 6.77 ms (profiles/r03/ab_mul_large.log); with the
+                              // in-register head 12 waves spill 5: 6.09 -> 5.93 ms per 2^17 products
+                              // (profiles/r03/ab_mul_large_w12.log)
 #endif
 template <int PS, bool BHAT>
 constexpr int mul_large_waves()
