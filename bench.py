@@ -7,6 +7,13 @@ n = 2048, qTESLA-p-III (q = 856145921), batch = 2^20 polynomials per GPU
     python bench.py --config {1,2,3,4,5} ...                      # BASELINE configs
     torchrun --nproc-per-node N bench.py --gpus N ...             # one rank per GPU
 
+--gpus N > 1 without a launcher (no WORLD_SIZE in the environment): the
+process starts N fresh child ranks itself before it touches the GPU
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set),
+relays rank 0's JSON line and exits with the worst child status.  Every rank
+needs a device of its own: fewer visible devices than ranks is an error
+unless --allow-shared-devices (the world-size-2 rehearsal on a one-GPU box).
+
   config 1  single forward NTT n=1024 p-I: the reference's serial CPU path
             (plumbing); the GPU line is the batch-1 launch latency
   config 2  forward NTT n=1024 p-I, batch 65536
@@ -75,6 +82,61 @@ def dist_env():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     return rank, world, local
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(nranks: int, argv: list[str]) -> int:
+    """Launcher-free multi-GPU run: start `nranks` fresh child processes of
+    this script, one per GPU, with the torch.distributed env set.  Called
+    before this process makes any GPU call (it never initialises HIP: the
+    children do).  Rank 0 inherits stdout and prints the one JSON line; if a
+    rank fails, the others are stopped (by PID) and the worst status is
+    returned."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(nranks):
+        env = {**os.environ, "RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nranks),
+               "LOCAL_WORLD_SIZE": str(nranks), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+               "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")}
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    worst = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0:
+                worst = worst or rc
+                for o in live:          # a failed rank would leave the others waiting in a barrier
+                    o.terminate()
+        if live:
+            time.sleep(0.05)
+    return worst if worst >= 0 else 128 - worst
+
+
+def check_devices(world: int, allow_shared: bool) -> int | None:
+    """One device per rank, or exit status 3 with the reason (unless shared
+    devices were asked for).  Counting devices does not initialise HIP."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        print("error: no GPU visible (the product has no CPU path)", file=sys.stderr)
+        return 3
+    if ndev < world and not allow_shared:
+        print(f"error: {world} ranks but only {ndev} visible device(s); every rank needs its own GPU "
+              f"(--allow-shared-devices runs ranks on shared devices, for rehearsals only)", file=sys.stderr)
+        return 3
+    return None
 
 
 class Dist:
@@ -201,6 +263,8 @@ def main():
                     help="p-III-4096 / p-III-8192: the n > 2048 four-step transforms (fwd / inv / fwdinv only)")
     ap.add_argument("--batch", type=int, default=None, help="polynomials per GPU")
     ap.add_argument("--ring", default=None, choices=["q", "m32"], help="--op nussbaumer: mod q or mod 2^32-1")
+    ap.add_argument("--allow-shared-devices", action="store_true",
+                    help="let ranks share devices when fewer than --gpus are visible (one-GPU rehearsals only)")
     ap.add_argument("--dist-backend", default="gloo", choices=["gloo", "nccl"],
                     help="process group for the barrier / max-over-ranks only (no data-path collective, so "
                          "gloo on CPU tensors by default; nccl = RCCL)")
@@ -217,15 +281,24 @@ def main():
     args.batch = args.batch or c_batch
     args.ring = args.ring or c_ring
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    rank, world, local = dist_env()
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
+    rc = check_devices(world, args.allow_shared_devices)
+    if rc is not None:
+        sys.exit(rc)
+
     import torch
     import ntt_amd
 
-    rank, world, local = dist_env()
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    # one rank per GPU; ranks beyond the visible devices share them (the
-    # world-size-2 rehearsal on a one-GPU box, with --dist-backend gloo)
-    dev_index = local % max(1, torch.cuda.device_count())
+    # one rank per GPU; with --allow-shared-devices ranks beyond the visible
+    # devices share them (the world-size-2 rehearsal on a one-GPU box)
+    dev_index = local % torch.cuda.device_count()
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     dist = Dist(world, args.dist_backend, device)
@@ -292,12 +365,6 @@ def main():
     dist.barrier()
     elapsed = dist.max(t1 - t0)
     fastest = dist.min(t1 - t0)
-    expiries = None
-    if args.param in ("p-III-4096", "p-III-8192"):
-        # the n > 2048 kernels' slot barriers: an expired wait poisons its
-        # polynomial (sentinel output) and counts here; any count fails the run
-        torch.cuda.synchronize(device)
-        expiries = ntt_amd.sync_expiries()
 
     if single:
         per_kind = {kinds[0]: evs[0][0][0].elapsed_time(evs[0][0][1]) / args.steps}
@@ -312,6 +379,14 @@ def main():
     check = {"roundtrip_identity_full_batch": None, "sampled_vs_oracle": None}
     if not args.no_check:
         check = checker_legs(args, ntt_amd, torch, x, y, z, first, count, n)
+    expiries = None
+    if ntt_amd.param_info(args.param)["n"] > 2048:
+        # the n > 2048 kernels' slot barriers: an expired wait poisons its
+        # polynomial (sentinel output) and counts here, read after the timed
+        # region AND the checker legs' own launches; any count fails the run
+        torch.cuda.synchronize(device)
+        expiries = ntt_amd.sync_expiries()
+    if not args.no_check:
         bad = 0.0 if all(v is None or v is True or (isinstance(v, dict) and v.get("ok")) for v in check.values()) \
             else 1.0
         if expiries:

@@ -7,19 +7,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 
 #include "../../include/qtesla_ntt.h"
 #include "dev_tables.hpp"
 #include "ntt_device.hpp"
 #include "ntt_large.hpp"
-#ifndef NTT_WGP
-#define NTT_WGP 0   // n = 2048 poly_ntt / poly_invntt on the workgroup-per-polynomial kernels (ntt_wg.hpp):
-                    // 1 persistent, 2 one polynomial per workgroup, 0 off
-#endif
-#if NTT_WGP
-#include "ntt_wg.hpp"   // measured slower; A/B builds only
-#endif
 #include "ntt_internal.h"
 #include "params.hpp"
 #include "pset.hpp"
@@ -56,12 +50,14 @@ const Tables &cpu_tables(int ps)
 
 // Per-device state: tables uploaded (retried after a failed attempt, e.g. a
 // first call made while another stream was being captured) and the launch
-// geometry of the device.
+// geometry of the device.  `ready` is published with release order once both
+// are done, so every later call on that device -- from any host thread, on
+// any stream -- takes the lock-free acquire-load path; only a device's first
+// calls serialise on g_dev_mutex (a thread-per-GPU host never contends after
+// its device's first call).
 struct DevInfo {
-    bool tables = false;
-    bool geo = false;
+    std::atomic<bool> ready{false};
     int cus = 256;
-    int wgp_occ = 4;   // resident k_wg_xform workgroups per CU (occupancy API)
 };
 std::mutex g_dev_mutex;
 DevInfo g_dev[kMaxDev];
@@ -73,23 +69,16 @@ int device_ready(DevInfo **out)
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_err(e);
     if (dev < 0 || dev >= kMaxDev) return hip_err(hipErrorInvalidDevice);
-    std::lock_guard<std::mutex> lk(g_dev_mutex);
     DevInfo &d = g_dev[dev];
-    if (!d.geo) {
-        hipDeviceProp_t prop;
-        if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return hip_err(e);
-        d.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-#if NTT_WGP
-        int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_wg_xform<2, false, (NTT_WGP == 1)>, WGP_T, 0) == hipSuccess &&
-            occ > 0)
-            d.wgp_occ = occ;
-#endif
-        d.geo = true;
-    }
-    if (!d.tables) {
-        if ((e = upload_device_tables(&cpu_tables(0))) != hipSuccess) return hip_err(e);
-        d.tables = true;
+    if (!d.ready.load(std::memory_order_acquire)) {
+        std::lock_guard<std::mutex> lk(g_dev_mutex);
+        if (!d.ready.load(std::memory_order_relaxed)) {
+            hipDeviceProp_t prop;
+            if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return hip_err(e);
+            d.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+            if ((e = upload_device_tables(&cpu_tables(0))) != hipSuccess) return hip_err(e);
+            d.ready.store(true, std::memory_order_release);
+        }
     }
     *out = &d;
     return NTT_OK;
@@ -147,7 +136,7 @@ int finish_launch()
 }
 
 template <template <int> class Launcher, class... Args>
-int dispatch(int ps, Args... args)
+int dispatch(int ps, Args &&...args)
 {
     switch (ps) {
     case 0: return Launcher<0>::run(args...);
@@ -196,20 +185,6 @@ template <int PS> struct LXform {
                 break;
             }
         } else {
-#if NTT_WGP
-            if constexpr (PSel<PS>::T::N == 2048) {
-                // n = 2048 natural-order transforms: one polynomial per
-                // persistent 512-thread workgroup (ntt_wg.hpp)
-                if (k == FWD || k == INV) {
-                    constexpr bool PERSIST = NTT_WGP == 1;
-                    const size_t res = PERSIST ? (size_t)d.cus * d.wgp_occ : batch;
-                    const dim3 g((uint32_t)(batch < res ? batch : res)), b(WGP_T);
-                    if (k == FWD) hipLaunchKernelGGL((k_wg_xform<PS, false, PERSIST>), g, b, 0, s, in, out, (uint32_t)batch);
-                    else hipLaunchKernelGGL((k_wg_xform<PS, true, PERSIST>), g, b, 0, s, in, out, (uint32_t)batch);
-                    return finish_launch();
-                }
-            }
-#endif
             const Launch l = launch_for(OP_XFORM, PS, batch, d);
             const dim3 g(l.grid), b(NTT_WG);
             const uint32_t nb = (uint32_t)batch;

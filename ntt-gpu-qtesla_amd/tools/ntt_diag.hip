@@ -11,6 +11,9 @@
 //              or dwordx4 (variant 1) accesses
 //   op 3       k_poly_mul (d_out = in * in): variant 0 full, 1 global loads +
 //              stores only, 2 arithmetic + LDS only (k_poly_mul's VAR)
+//   op 4       the round-3 workgroup-per-polynomial n = 2048 transforms
+//              (ntt_wg.hpp): variant 0 / 1 forward persistent /
+//              one polynomial per workgroup, 2 / 3 the same inverses
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -19,6 +22,7 @@
 #include "../../include/qtesla_ntt.h"
 #include "../csrc/dev_tables.hpp"
 #include "../csrc/ntt_device.hpp"
+#include "ntt_wg.hpp"
 
 namespace qntt {
 namespace {
@@ -172,6 +176,25 @@ extern "C" int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uin
         const dim3 g2((uint32_t)g_cus * 2);
         if (variant == 0) hipLaunchKernelGGL((k_copy_diag<1>), g2, dim3(512), 0, s, d_in, d_out, (uint32_t)batch);
         else hipLaunchKernelGGL((k_copy_diag<4>), g2, dim3(512), 0, s, d_in, d_out, (uint32_t)batch);
+        return hipGetLastError() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    }
+    if (op == 4) {   // workgroup-per-polynomial kernels (p-III only)
+        if (ps != 2) return NTT_ERR_PARAM;
+        const bool persist = !(variant & 1);
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_wg_xform<2, false, true>, WGP_T, 0) !=
+                hipSuccess || occ < 1)
+            occ = 4;
+        const size_t res = persist ? (size_t)g_cus * occ : batch;
+        const dim3 g((uint32_t)(batch < res ? batch : res)), b(WGP_T);
+        const uint32_t nb = (uint32_t)batch;
+        switch (variant) {
+        case 0: hipLaunchKernelGGL((k_wg_xform<2, false, true>), g, b, 0, s, d_in, d_out, nb); break;
+        case 1: hipLaunchKernelGGL((k_wg_xform<2, false, false>), g, b, 0, s, d_in, d_out, nb); break;
+        case 2: hipLaunchKernelGGL((k_wg_xform<2, true, true>), g, b, 0, s, d_in, d_out, nb); break;
+        case 3: hipLaunchKernelGGL((k_wg_xform<2, true, false>), g, b, 0, s, d_in, d_out, nb); break;
+        default: return NTT_ERR_PARAM;
+        }
         return hipGetLastError() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
     }
     if (op != 0 && op != 1 && op != 3) return NTT_ERR_PARAM;

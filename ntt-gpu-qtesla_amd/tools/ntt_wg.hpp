@@ -1,6 +1,8 @@
 // ntt_wg.hpp -- gfx950 n = 2048 transforms with one polynomial per 512-thread
-// workgroup (round 3).  Included by ntt_kernels.hip after
-// ntt_device.hpp (it owns the twiddle tables c_fwd2 / c_inv2).
+// workgroup (round 3 experiment; measured slower than the
+// wave-per-polynomial kernels, so it lives in the tools-only diag library:
+// ntt_diag.hip op 4).  Included after ntt_device.hpp (it owns the twiddle
+// tables c_fwd2 / c_inv2).
 //
 // Why this shape: measured on MI355X (profiles/r03/), an in-place stream in
 // which every wave moves ONE 1 KiB piece (4 dwords per lane) runs at the
@@ -41,7 +43,7 @@
 // p = blockIdx + i gridDim, the next polynomial's 4 words prefetched into
 // registers while the current one is transformed.
 #pragma once
-#include "ntt_device.hpp"
+#include "../csrc/ntt_device.hpp"
 
 namespace qntt {
 

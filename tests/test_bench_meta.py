@@ -39,6 +39,31 @@ def test_pmc_entry_sane(ntt, op, param, batch, ring):
     assert 0.99 * alg < e["hbm_bytes_per_launch"] < 1.1 * alg, (e["hbm_bytes_per_launch"], alg)
 
 
+def _tree_hash():
+    """SRC_HASH of the sources in this tree, as the Makefile computes it."""
+    import subprocess
+    out = subprocess.run(["make", "-s", "-n", "-p", "-C", os.path.join(ROOT, "ntt-gpu-qtesla_amd")],
+                         capture_output=True, text=True).stdout
+    for line in out.splitlines():
+        if line.startswith("SRC_HASH := ") and len(line.split()[-1]) == 16:
+            return line.split()[-1]
+    return None
+
+
+def test_pmc_summary_matches_tree_build():
+    """Non-blocking staleness check: the committed PMC summary should have been
+    measured on the library these sources build.  A source edit without a new
+    measurement xfails here (bench.py then reports traffic: null)."""
+    with open(bench.PMC_PATH) as f:
+        entries = json.load(f)["entries"]
+    tree = _tree_hash()
+    if tree is None:
+        pytest.skip("make -p did not report SRC_HASH")
+    stale = sorted({e.get("build_hash") for e in entries.values()} - {tree})
+    if stale:
+        pytest.xfail(f"profiles/pmc_summary.json measured on build(s) {stale}, the tree builds {tree}")
+
+
 def test_load_pmc_reports_stale_build(ntt):
     """A hash mismatch yields traffic None plus the reason, never a stale number."""
     op, param, batch, ring = bench.CONFIGS[3]

@@ -49,3 +49,31 @@ def test_gloo_world2_sharding():
     whole = O.poly_ntt(O.fill_uniform(6, "p-I", 0x5EED0002, 0), "p-I")
     got = np.concatenate([np.frombuffer(out[r][3], np.uint32).reshape(-1, 1024) for r in range(world)])
     assert np.array_equal(got, whole)
+
+
+def test_bench_launcher_free_ranks_fail_loudly_without_devices():
+    """bench.py --gpus 2 with no launcher starts its own two ranks; with fewer
+    visible devices than ranks (none here) every rank exits non-zero and so
+    does the parent -- it never falls back to measuring fewer GPUs."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--batch", "64",
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode != 0
+    assert "error:" in r.stderr, r.stderr       # the failing rank says why (the others are stopped)
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_rejects_launcher_world_mismatch():
+    """Under a launcher, --gpus must equal WORLD_SIZE."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {**os.environ, "WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--batch", "64",
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr

@@ -109,7 +109,8 @@ def test_large_nussbaumer_unsupported(ntt, dev):
 @pytest.mark.parametrize("batch", [1, 2, 5, 7, 64, 389])
 def test_large_poly_mul_random(ntt, oracle, dev, ps, batch):
     """Fused product (k_poly_mul_large): partial and full workgroup steps
-    (SLOTS = 6 / 2 polynomials per step), bit-exact against the oracle."""
+    (SLOTS = 6 / 3 polynomials per step on the 12-wave workgroups), bit-exact
+    against the oracle."""
     a = oracle.fill_uniform(batch, ps, 0x3A + batch, 0)
     b = oracle.fill_uniform(batch, ps, 0x3B + batch, 0)
     ta, tb = _dev(ntt, a, dev), _dev(ntt, b, dev)

@@ -1,5 +1,5 @@
 """CPU model of the workgroup-per-polynomial n = 2048 transforms
-(ntt-gpu-qtesla_amd/csrc/ntt_wg.hpp, A/B builds only -- DESIGN.md §7a): the
+(ntt-gpu-qtesla_amd/tools/ntt_wg.hpp, tools-only diag library -- DESIGN.md §7a): the
 six pass layouts and five LDS exchange maps are bijective, every register's
 address is a fixed offset from one per-thread base (the offsets the kernel
 hard-codes), every access is bank-conflict-free per half-wave, and the
