@@ -55,6 +55,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ntt-gpu-qtesla_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_CLOCK_GHZ = 2.4         # MI355X peak engine clock
+SIMDS_PER_CU = 4
+# ops whose dominant kernel is bound by VALU issue, not HBM:
+# their line's roofline is the VALU one, the HBM fraction a secondary field
+VALU_BOUND = {"polymul", "polymul_ntt", "nussbaumer"}
 METRIC = "NTTs/sec (fwd+inv, n=2048 qTESLA-p-III) at batch=2^20; achieved HBM GB/s"
 SEED = 0x5EED0003
 PMC_PATH = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -243,6 +248,43 @@ def load_pmc(workload: str, batch: int, build_hash: str):
     return e.get("hbm_bytes_per_launch"), "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, this build"
 
 
+def load_valu(workload: str, batch: int, build_hash: str, kernel_key: str):
+    """VALU issue demand per launch of the dominant kernel (SIMD-cycles, from
+    SQ_INSTS_VALU x the kernel's opcode mix weighted by the measured issue
+    costs, tools/valu_summary.py), only when measured on this build."""
+    try:
+        with open(PMC_PATH) as f:
+            e = json.load(f).get("entries", {}).get(workload)
+    except (OSError, ValueError):
+        return None, "no profiles/pmc_summary.json"
+    if e is None or "valu" not in e:
+        return None, "no VALU counter entry for this workload"
+    if e.get("batch") != batch:
+        return None, f"VALU entry measured at batch {e.get('batch')}"
+    if e.get("build_hash") != build_hash:
+        return None, f"VALU entry measured on build {e.get('build_hash')}, this library is {build_hash}"
+    k = e["valu"]["kernels"].get(kernel_key)
+    if k is None:
+        return None, f"no VALU entry for kernel {kernel_key}"
+    return dict(k, cus=e["valu"].get("cus", 256)), "rocprofv3 SQ_INSTS_VALU x opcode-mix issue cost, this build"
+
+
+def valu_roofline(v, launch_ms: float, hbm: dict) -> dict:
+    """achieved = VALU issue SIMD-cycles per launch / live launch time;
+    peak = 4 SIMDs x CUs x 2.4 GHz; frac_at_held_clock uses the clock the
+    counter pass measured (GRBM_GUI_ACTIVE / 8 XCDs / kernel time)."""
+    if v is None:
+        return {"bound": "valu", "achieved": None, "peak": None, "unit": "G SIMD-cycles/s", "frac": None, "hbm": hbm}
+    cyc = v["valu_simd_cycles_per_launch"]
+    achieved = cyc / (launch_ms * 1e-3) / 1e9
+    peak = SIMDS_PER_CU * v["cus"] * PEAK_CLOCK_GHZ
+    held = SIMDS_PER_CU * v["cus"] * v["clock_ghz_pmc"]
+    return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G SIMD-cycles/s", "frac": achieved / peak,
+            "frac_at_held_clock": achieved / held, "clock_ghz_pmc": v["clock_ghz_pmc"],
+            "valu_insts_per_launch": v["SQ_INSTS_VALU"], "mean_simd_cycles_per_valu": v["mean_simd_cycles_per_valu"],
+            "valu_simd_cycles_per_launch": cyc, "hbm": hbm}
+
+
 def workload_name(op, param, n, q, ring):
     base = {"fwdinv": "fwd+inv negacyclic NTT", "fwd": "forward negacyclic NTT", "inv": "inverse negacyclic NTT",
             "polymul": "fused negacyclic poly-mul",
@@ -401,6 +443,16 @@ def main():
     unit = UNIT[args.op]
     build_hash = ntt_amd.build_hash()
     traffic, traffic_note = load_pmc(workload, count, build_hash)
+    hbm = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
+           "avg_launch_ms": per_kind[dom], "alg_bytes_per_launch": alg_bytes,
+           "timing": "region events / steps" if single else "per-launch events", "per_kernel_ms": per_kind}
+    if args.op in VALU_BOUND:
+        v, v_note = load_valu(workload, count, build_hash, dom)
+        roofline = dict(valu_roofline(v, per_kind[dom], hbm), kernel=dom, valu_note=v_note,
+                        avg_launch_ms=per_kind[dom], per_kernel_ms=per_kind)
+    else:
+        roofline = hbm
     headline = args.op == "fwdinv" and args.param == "p-III" and args.batch == 1 << 20
     out = {
         "metric": METRIC if headline else f"{unit} ({workload}, batch {args.batch} per GPU)",
@@ -421,11 +473,7 @@ def main():
                    "batch_per_gpu": count, "global_batch": world * count, "parallelism": f"batch-shard x{world}",
                    "dist_backend": args.dist_backend if world > 1 else None},
         "hbm_gbs_algorithmic": value * n * (bytes_per_coeff if args.op != "fwdinv" else 16) / 1e9,
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
-                     "avg_launch_ms": per_kind[dom], "alg_bytes_per_launch": alg_bytes,
-                     "timing": "region events / steps" if single else "per-launch events",
-                     "per_kernel_ms": per_kind},
+        "roofline": roofline,
         "check": check,
         "build": {"hash": build_hash},
         "cpu_baseline": None,

@@ -71,3 +71,28 @@ def test_load_pmc_reports_stale_build(ntt):
     workload = bench.workload_name(op, param, info["n"], info["q"], ring)
     traffic, note = bench.load_pmc(workload, batch, "0000000000000000")
     assert traffic is None and "this library is 0000000000000000" in note
+
+
+def test_valu_roofline_fields():
+    """VALU-bound ops report roofline.bound "valu": SIMD issue cycles per
+    launch (SQ_INSTS_VALU x mean opcode cost) over the live launch time,
+    against 4 SIMDs x CUs x 2.4 GHz, with the HBM fraction kept beside it."""
+    v = {"valu_simd_cycles_per_launch": 1024 * 2.4e9 * 5e-3, "clock_ghz_pmc": 2.0, "cus": 256,
+         "SQ_INSTS_VALU": 1.0, "mean_simd_cycles_per_valu": 3.5}
+    r = bench.valu_roofline(v, 10.0, {"bound": "hbm", "frac": 0.4})
+    assert r["bound"] == "valu" and r["unit"] == "G SIMD-cycles/s"
+    assert abs(r["frac"] - 0.5) < 1e-12 and abs(r["frac_at_held_clock"] - 0.6) < 1e-12
+    assert r["hbm"]["frac"] == 0.4
+    assert bench.valu_roofline(None, 10.0, {})["frac"] is None
+    assert {"polymul", "polymul_ntt", "nussbaumer"} == bench.VALU_BOUND
+
+
+def test_valu_cost_table_classes():
+    """The committed issue-cost table (tools/valu_cost.hip under rocprofv3):
+    the VOP2 add/sub/logic ops issue at about twice the rate of min/max and
+    the multiply class, which is what the poly_mul / Nussbaumer VALU roofline weights by."""
+    with open(os.path.join(ROOT, "profiles", "valu_issue_cost.json")) as f:
+        cost = json.load(f)["cost"]
+    assert cost["v_add_u32"] < 3.0 and cost["v_sub_u32"] < 3.0
+    for op in ("v_min_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u64_u32", "v_mad_i64_i32"):
+        assert 4.0 < cost[op] < 5.0, op

@@ -76,6 +76,10 @@ for step in "$@"; do
         sq_c*) c=${step#sq_c}; run sq_c$c 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sq_c$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-check ;;
         sqb_c*) c=${step#sqb_c}; run sqb_c$c 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM --output-format csv -d gpurun_out/sqb_c$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-check ;;
         listpmc) run listpmc 60 rocprofv3 -L ;;
+        # VALU roofline inputs (tools/valu_summary.py): per-opcode issue cost, and
+        # SQ_INSTS_VALU + GRBM_GUI_ACTIVE per launch of a config's kernel
+        valucost) run valucost 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU --output-format csv -d gpurun_out/valucost -o run -- ./ntt-gpu-qtesla_amd/bin/valu_cost 16384 ;;
+        valu_c*) c=${step#valu_c}; run valu_c$c 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valu_c$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
