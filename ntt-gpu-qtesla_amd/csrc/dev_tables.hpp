@@ -13,6 +13,7 @@
 
 #include "ntt_device.hpp"
 #include "ntt_large.hpp"
+#include "ntt_big.hpp"
 #include "params.hpp"
 
 namespace qntt {
@@ -145,6 +146,40 @@ inline hipError_t upload_large_tables(int ps, const Tables &t)
     return hipMemcpyToSymbol(HIP_SYMBOL(c_lastinv), last, sizeof last, (size_t)idx * sizeof last, hipMemcpyHostToDevice);
 }
 
+// Tables of the wave-per-polynomial n = 4096 / 8192 transforms (ntt_big.hpp):
+// the uniform pass-1 twiddles k < R and the LDS image (lane table of every
+// chunk, then the bit-5 table), tests/test_big_dataflow.py::lane_k
+inline hipError_t upload_big_tables(int ps, const Tables &t)
+{
+    const ParamSet &p = *param_set(ps);
+    const int idx = ps - LARGE_PS0;
+    const uint32_t L = p.logn, R = 1u << (L - 6), NC = L - 11, CH = 1u << NC;
+    hipError_t e;
+    for (int inv = 0; inv < 2; inv++) {
+        uint2 tw[BIG_RMAX] = {};
+        for (uint32_t k = 0; k < R; k++) dev_pair(p, t, inv != 0, k, tw[k].x, tw[k].y);
+        if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_bigtw), tw, sizeof tw, (size_t)(idx * 2 + inv) * sizeof tw,
+                                   hipMemcpyHostToDevice)) != hipSuccess)
+            return e;
+        const uint32_t lane_pairs = TW2_ENTRIES * 64 * CH;
+        std::vector<uint32_t> o(2 * (lane_pairs + R), 0);
+        auto put = [&](uint32_t slot, uint32_t k) { dev_pair(p, t, inv != 0, k, o[2 * slot], o[2 * slot + 1]); };
+        for (uint32_t c = 0; c < CH; c++)
+            for (int ent = 0; ent < TW2_ENTRIES; ent++) {
+                const int b = ent < 1 ? 4 : ent < 3 ? 3 : ent < 7 ? 2 : ent < 15 ? 1 : 0;
+                const uint32_t m = ent - ((1u << (4 - b)) - 1);
+                for (uint32_t lane = 0; lane < 64; lane++)
+                    put((c * TW2_ENTRIES + ent) * 64 + lane,
+                        (1u << (L - 1 - b)) + ((c + (bitrev(lane, 6) << NC)) << (4 - b)) + m);
+            }
+        for (uint32_t i = 0; i < R; i++) put(lane_pairs + i, R + i);   // bit-5 stage: k = 2^M + m + H h
+        if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_bigimg), o.data(), o.size() * 4,
+                                   (size_t)(idx * 2 + inv) * BIG_IMG_VEC4_MAX * 16, hipMemcpyHostToDevice)) != hipSuccess)
+            return e;
+    }
+    return hipSuccess;
+}
+
 // Upload every table of the parameter sets to the current device.
 inline hipError_t upload_device_tables(const Tables *tabs /* [NPARAM_SETS] */)
 {
@@ -163,8 +198,9 @@ inline hipError_t upload_device_tables(const Tables *tabs /* [NPARAM_SETS] */)
             if (e != hipSuccess) return e;
         }
     for (int ps = LARGE_PS0; ps < LARGE_PS0 + LARGE_NPS; ps++) {
-        const hipError_t e = upload_large_tables(ps, tabs[ps]);
+        hipError_t e = upload_large_tables(ps, tabs[ps]);
         if (e != hipSuccess) return e;
+        if ((e = upload_big_tables(ps, tabs[ps])) != hipSuccess) return e;
     }
     return hipSuccess;
 }

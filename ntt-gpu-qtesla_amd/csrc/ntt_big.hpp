@@ -1,0 +1,328 @@
+// ntt_big.hpp -- gfx950 n = 4096 / 8192 transforms with ONE WAVE PER
+// POLYNOMIAL (param sets 3 / 4, p-III's prime; SURVEY.md 8f row 3, larger n;
+// the reference's alternatives for other sizes are its Stockham kernels,
+// NTT.cu:1085-1153 / 1268-1337).  Included by ntt_kernels.hip after
+// ntt_large.hpp.
+//
+// The n = 2048 kernels' geometry, widened: every lane holds R = n/64
+// coefficients in VGPRs (64 / 128), so a polynomial never leaves its wave --
+// no cross-wave exchange, no slot barrier, no sub-tree scaling.  With
+// L = log2 n, M = L - 6 register bits, H = R/2, NC = L - 11 chunk bits
+// (tests/test_big_dataflow.py models every map below against the oracle):
+//   A   load / pass 1: lane = pos 0..5, register j = pos 6..L-1.  The M CT
+//       stages on pos L-1 .. 6 run in registers with wave-uniform twiddles
+//       (scalar loads, k < R).
+//   bit-5 stage: v_permlane32_swap of registers j, j + H exchanges lane bit 5
+//       (pos 5) with register bit M-1 (pos L-1); the butterfly's twiddle
+//       depends on the lane half (LDS table of R pairs).  Layout A'': lane =
+//       pos 0..4 + pos L-1, register j: bits 0..M-2 = pos 6..L-2, bit M-1 =
+//       pos 5.
+//   chunks: c = (pos 5 .. 5+NC-1) selects 32 registers j(c, t) =
+//       (c >> 1) + 2^(NC-1) t + H (c & 1); each chunk is transposed through the
+//       wave's private 8 KiB LDS buffer (b32 writes, the n = 2048 kernels'
+//       b128 read side and XOR swizzle, conflict-free both ways) into
+//   B   pass 2 / store: lane l with bit i = pos L-1-i, register j' = pos 0..4:
+//       the five CT stages on pos 4..0 with per-lane twiddles (the chunk's
+//       lane-major LDS table), then natural index brv_L(pos) =
+//       brv5(j') 2^(L-5) + brv_NC(c) 64 + l: every store is a lane-contiguous
+//       256-B run, chunk by chunk (the stores of chunk c overlap chunk c+1's
+//       transpose and arithmetic).
+// The inverse runs the mirror image (B loads, GS pass 2 and transposes per
+// chunk, the GS bit-5 stage and swap back, the GS stages on pos 6..L-1, the
+// last one scaled by n^-1, A stores).
+//
+// LDS: one workgroup per CU -- WAVES 8 KiB transpose buffers plus the
+// direction's table image (31 x 2^NC lane entries + R bit-5 pairs):
+//   n = 4096: 16 waves x 8 KiB + 31.75 KiB (4 waves per SIMD, <= 128 VGPRs)
+//   n = 8192: BIG_WAVES_8192 x 8 KiB + 63 KiB
+#pragma once
+#include <utility>
+
+#include "ntt_large.hpp"
+
+namespace qntt {
+
+// Compile-time loop: f(integral_constant<int, 0>) ... f(<N-1>).  The n = 8192
+// bodies (128 registers, ~10k instructions) pass LLVM's pragma-unroll
+// threshold, and a partly rolled loop indexes the register array at run time
+// (scratch memory, ~7x slower, measured); this expansion cannot fail.
+template <class F, int... I>
+__device__ __forceinline__ void sfor_impl(F &&f, std::integer_sequence<int, I...>)
+{
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F &&f)
+{
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+#ifndef BIG_WAVES_8192
+#define BIG_WAVES_8192 8   // n = 8192: 128 data VGPRs (217 / 205 in all): 8 waves = 2 per SIMD
+#endif
+
+constexpr int BIG_RMAX = 128;
+constexpr int BIG_IMG_VEC4_MAX = (TW2_ENTRIES * 64 * 4 + BIG_RMAX) * 2 / 4;   // n = 8192 image, uint4
+
+// wave-uniform pass-1 twiddles k < R, [set][fwd/inv][k] (device conventions)
+__constant__ uint2 c_bigtw[LARGE_NPS][2][BIG_RMAX];
+// per-workgroup LDS images: lane table [c][e][lane] (e as TW2_ENTRIES), then
+// the R bit-5 pairs, [set][fwd/inv]
+__device__ uint4 g_bigimg[LARGE_NPS][2][BIG_IMG_VEC4_MAX];
+
+template <int PS>
+struct Big {
+    using PL = typename PSel<PS>::T;   // the n-point set
+    using P = PS2;                     // same prime; butterflies only use Q
+    static_assert(PL::Q == P::Q, "large-n sets use p-III's prime");
+    static constexpr int L = PL::LOGN;
+    static constexpr int M = L - 6;
+    static constexpr int R = 1 << M;
+    static constexpr int H = R / 2;
+    static constexpr int NC = L - 11;
+    static constexpr int CH = 1 << NC;
+    static constexpr int IDX = PS - LARGE_PS0;
+    static constexpr int WAVES = L == 12 ? 16 : BIG_WAVES_8192;
+    static constexpr int NT = WAVES * 64;
+    static constexpr int OCC = (WAVES + 3) / 4;                   // waves per SIMD
+    static constexpr int LANE_PAIRS = TW2_ENTRIES * 64 * CH;      // lane table
+    static constexpr int IMG_WORDS = 2 * (LANE_PAIRS + R);         // + bit-5 table
+    static constexpr int IMG_VEC4 = IMG_WORDS / 4;
+    static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + IMG_WORDS;
+    static_assert(IMG_VEC4 <= BIG_IMG_VEC4_MAX, "image size");
+    static_assert(LDS_WORDS * 4 <= 160 * 1024, "one workgroup per CU");
+    // register of transposition row t of chunk c (layout A'')
+    static __host__ __device__ constexpr int creg(int c, int t) { return (c >> 1) + (1 << (NC - 1)) * t + H * (c & 1); }
+    // word offset of B register j' of chunk c from the lane's natural-order base
+    static __host__ __device__ constexpr uint32_t boff(int c, int jp)
+    {
+        return (brv5(jp) << (L - 5)) + ((NC == 2 ? (((c & 1) << 1) | (c >> 1)) : c) << 6);
+    }
+};
+
+// A'' -> LDS address of transposition row t (b32, conflict-free per 32-lane
+// group): the chunk-local position P = (l & 31) + 32 t + 1024 h through the
+// n = 2048 swizzle (tests/test_big_dataflow.py::w_addr)
+__device__ __forceinline__ uint32_t big_waddr(uint32_t wb, int t)
+{
+    return (wb ^ xm_of((uint32_t)t)) + 32u * ((uint32_t)t ^ (((uint32_t)t >> 2) & 1u));
+}
+__device__ __forceinline__ uint32_t big_wbase(uint32_t lane)
+{
+    const uint32_t h = lane >> 5;
+    return ((lane & 31u) ^ (h << 4)) + 1024u * h;
+}
+
+// the R words of a lane at compile-time offsets from one base pointer
+template <int NR, class Off>
+__device__ __forceinline__ void load32n(uint32_t (&r)[NR], const uint32_t *src, Off off)
+{
+    sfor<NR>([&](auto J) { r[J] = ld_in(src + off(J)); });
+}
+
+// chunk_loop with R registers: workgroup b owns polynomials [b WAVES ppw,
+// (b+1) WAVES ppw), its waves take consecutive ones (dispatch-ordered), the
+// first polynomial's loads are issued before the table prologue.  The kernels'
+// `load` / `process` lambdas are always_inline: the n = 8192 bodies are too
+// large for the inliner's heuristics, and an outlined body takes the register
+// array by reference (in scratch memory)
+template <class BG, class Prologue, class Load, class Process>
+__device__ __forceinline__ void big_loop(uint32_t npoly, uint32_t ppw, Prologue &prologue, Load &load, Process &process)
+{
+    uint32_t r[BG::R];
+    uint32_t u = blockIdx.x * (BG::WAVES * ppw) + wave_id();
+    if (u < npoly) load(r, u);
+    prologue();   // every wave reaches the barrier inside
+    if (u >= npoly) return;
+    process(r, u);
+#pragma unroll 1
+    for (uint32_t i = 1; i < ppw; ++i) {
+        u += BG::WAVES;
+        if (u >= npoly) break;
+        load(r, u);
+        process(r, u);
+    }
+}
+
+template <class BG, bool INV>
+__device__ __forceinline__ void fill_big_tw(uint32_t *tab)
+{
+    const uint4 *src = g_bigimg[BG::IDX][INV ? 1 : 0];
+    uint4 *dst = reinterpret_cast<uint4 *>(tab);
+    for (int i = threadIdx.x; i < BG::IMG_VEC4; i += BG::NT) dst[i] = src[i];
+}
+
+template <class BG>
+__device__ __forceinline__ const uint2 *big_tw(bool inv)
+{
+    return c_bigtw[BG::IDX][inv ? 1 : 0] + opaque_zero();
+}
+
+// forward pass 1: CT stages on pos L-1 .. 6 (register bits M-1 .. 0), twiddle
+// k = 2^s + (j >> (M - s)), uniform; inputs < 2q (stage 0 unreduced)
+template <class BG>
+__device__ __forceinline__ void big_fwd_pass1(uint32_t (&r)[BG::R])
+{
+    constexpr int M = BG::M;
+    sfor<M>([&](auto S) {
+        constexpr int s = S, hh = 1 << (M - 1 - s);
+        sfor<BG::R / 32>([&](auto B) {
+            const uint2 *tw = big_tw<BG>(false);   // <= 16 pairs in SGPRs at a time
+            sfor<32>([&](auto J) {
+                constexpr int j = 32 * B + J;
+                if constexpr ((j & hh) == 0) {
+                    const uint2 w = tw[(1 << s) + (j >> (M - s))];
+                    ct_bfly<BG::P::Q, (s > 0)>(r[j], r[j + hh], w.x, w.y);
+                }
+            });
+        });
+    });
+}
+
+// bit-5 stage (forward): swap lane bit 5 with register bit M-1, butterfly
+// with twiddle k = 2^M + m + H h from the LDS table `sw`
+template <class BG>
+__device__ __forceinline__ void big_fwd_bit5(uint32_t (&r)[BG::R], const uint2 *sw, uint32_t h)
+{
+    sfor<BG::H>([&](auto Mi) {
+        constexpr int m = Mi;
+        const auto pr = __builtin_amdgcn_permlane32_swap(r[m], r[m + BG::H], false, false);
+        r[m] = pr[0];
+        r[m + BG::H] = pr[1];
+        const uint2 w = sw[m + BG::H * h];
+        ct_bfly<BG::P::Q>(r[m], r[m + BG::H], w.x, w.y);
+    });
+}
+
+template <int PS>
+__global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_fwd_big(const uint32_t *in, uint32_t *out, uint32_t npoly,
+                                                                        uint32_t ppw)
+{
+    using BG = Big<PS>;
+    using P = typename BG::P;
+    constexpr uint32_t N = BG::PL::N;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BG::LDS_WORDS];
+    uint32_t *const tabw = lds + BG::WAVES * XPOSE_WORDS;
+    auto prologue = [&]() {
+        fill_big_tw<BG, false>(tabw);
+        __syncthreads();
+    };
+    const uint32_t lane = threadIdx.x & 63, h = lane >> 5;
+    uint32_t *const buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
+    const uint2 *const tab = reinterpret_cast<const uint2 *>(tabw);
+    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {   // layout A: natural, 256-B runs
+        uint32_t lo = lane;
+        asm volatile("" : "+v"(lo));
+        load32n<BG::R>(r, in + (size_t)u * N + lo, [](int j) { return 64u * (uint32_t)j; });
+    };
+    auto process = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
+        big_fwd_pass1<BG>(r);
+        big_fwd_bit5<BG>(r, tab + BG::LANE_PAIRS + opaque_zero(), h);
+        uint32_t lo = lane;   // opaque per unit: scalar base + 32-bit lane offset stores
+        asm volatile("" : "+v"(lo));
+        uint32_t *const dst = out + (size_t)u * N + lo;
+        sfor<BG::CH>([&](auto C) {
+            constexpr int c = C;
+            // transpose addresses recomputed per chunk from an opaque lane
+            // (not 16 loop-invariant address VGPRs)
+            const uint32_t wb = big_wbase(opaque_lane());
+            const Lane<P> LB(opaque_lane());   // the n = 2048 b128 read side (Lp = brv6(lane))
+            sfor<32>([&](auto T) { buf[big_waddr(wb, T)] = r[BG::creg(c, T)]; });
+            compiler_fence();
+            uint32_t v[32];
+            sfor<8>([&](auto Q) {
+                const uint4 x = *reinterpret_cast<const uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm));
+                v[4 * Q + 0] = x.x;
+                v[4 * Q + 1] = x.y;
+                v[4 * Q + 2] = x.z;
+                v[4 * Q + 3] = x.w;
+            });
+            compiler_fence();
+            fwd_pass2<P>(v, tab + TW2_ENTRIES * 64 * c + opaque_zero(), lane);
+            sfor<32>([&](auto JP) { st_out(dst + BG::boff(c, JP), canon4<P>(v[JP])); });
+        });
+    };
+    big_loop<BG>(npoly, ppw, prologue, load, process);
+}
+
+template <int PS>
+__global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const uint32_t *in, uint32_t *out, uint32_t npoly,
+                                                                        uint32_t ppw)
+{
+    using BG = Big<PS>;
+    using P = typename BG::P;
+    constexpr uint32_t N = BG::PL::N;
+    constexpr int M = BG::M, H = BG::H;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BG::LDS_WORDS];
+    uint32_t *const tabw = lds + BG::WAVES * XPOSE_WORDS;
+    auto prologue = [&]() {
+        fill_big_tw<BG, true>(tabw);
+        __syncthreads();
+    };
+    const uint32_t lane = threadIdx.x & 63, h = lane >> 5;
+    uint32_t *const buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
+    const uint2 *const tab = reinterpret_cast<const uint2 *>(tabw);
+    // layout B of every chunk, in the chunk's register slots j(c, j')
+    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
+        uint32_t lo = lane;
+        asm volatile("" : "+v"(lo));
+        const uint32_t *src = in + (size_t)u * N + lo;
+        sfor<BG::CH>([&](auto C) { sfor<32>([&](auto JP) { r[BG::creg(C, JP)] = ld_in(src + BG::boff(C, JP)); }); });
+    };
+    auto process = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
+        sfor<BG::CH>([&](auto C) {
+            constexpr int c = C;
+            const uint32_t wb = big_wbase(opaque_lane());   // per chunk (see the forward)
+            const Lane<P> LB(opaque_lane());
+            uint32_t v[32];
+            sfor<32>([&](auto JP) { v[JP] = r[BG::creg(c, JP)]; });
+            inv_pass2<P>(v, tab + TW2_ENTRIES * 64 * c + opaque_zero(), lane);
+            sfor<8>([&](auto Q) {
+                *reinterpret_cast<uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm)) =
+                    make_uint4(v[4 * Q + 0], v[4 * Q + 1], v[4 * Q + 2], v[4 * Q + 3]);
+            });
+            compiler_fence();
+            sfor<32>([&](auto T) { r[BG::creg(c, T)] = buf[big_waddr(wb, T)]; });
+            compiler_fence();
+        });
+        // bit-5 stage: GS with the lane-half twiddle, then swap back
+        const uint2 *sw = tab + BG::LANE_PAIRS + opaque_zero();
+        sfor<H>([&](auto Mi) {
+            constexpr int m = Mi;
+            const uint2 w = sw[m + H * h];
+            gs_bfly<P::Q>(r[m], r[m + H], w.x, w.y);
+            const auto pr = __builtin_amdgcn_permlane32_swap(r[m], r[m + H], false, false);
+            r[m] = pr[0];
+            r[m + H] = pr[1];
+        });
+        // GS stages on pos 6 .. L-2 (register bits 0 .. M-2), uniform twiddles
+        sfor<M - 1>([&](auto JB) {
+            constexpr int jb = JB, hh = 1 << jb, s = M - 1 - jb;
+            sfor<BG::R / 32>([&](auto B) {
+                const uint2 *tw = big_tw<BG>(true);   // <= 16 pairs in SGPRs at a time
+                sfor<32>([&](auto J) {
+                    constexpr int j = 32 * B + J;
+                    if constexpr ((j & hh) == 0) {
+                        const uint2 w = tw[(1 << s) + (j >> (jb + 1))];
+                        gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+                    }
+                });
+            });
+        });
+        // last stage (pos L-1) with n^-1: x' = (x + y) n^-1, y' = (x - y) n^-1 psi^-brv(1)
+        constexpr uint32_t S0 = BG::PL::NINV, S0P = cshoup(S0, P::Q);
+        constexpr TwPair S1 = csigned_tw(BG::PL::C1, P::Q);
+        uint32_t lo = lane;
+        asm volatile("" : "+v"(lo));
+        uint32_t *const dst = out + (size_t)u * N + lo;
+        sfor<H>([&](auto J) {
+            constexpr int j = J;
+            const uint32_t x = r[j], y = r[j + H];
+            st_out(dst + 64u * j, csub<P::Q>(shoup_mul<P::Q>(x + y, S0, S0P)));
+            st_out(dst + 64u * (j + H), csub<P::Q>(sshoup_mul<P::Q>(x - y, S1.x, S1.y)));
+        });
+    };
+    big_loop<BG>(npoly, ppw, prologue, load, process);
+}
+
+}  // namespace qntt

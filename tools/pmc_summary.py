@@ -33,8 +33,8 @@ def load(path):
 
 def kernel_patterns(op, ps, ring):
     if ps >= 3:   # n = 4096 / 8192: the multi-wave four-step kernels
-        return {"fwdinv": {"fwd": f"k_ntt_fwd_large<{ps}>", "inv": f"k_ntt_inv_large<{ps}>"},
-                "fwd": {"fwd": f"k_ntt_fwd_large<{ps}>"}, "inv": {"inv": f"k_ntt_inv_large<{ps}>"},
+        return {"fwdinv": {"fwd": f"k_ntt_fwd_big<{ps}>", "inv": f"k_ntt_inv_big<{ps}>"},
+                "fwd": {"fwd": f"k_ntt_fwd_big<{ps}>"}, "inv": {"inv": f"k_ntt_inv_big<{ps}>"},
                 "polymul": {"mul": f"k_poly_mul_large<{ps}, false>"},
                 "polymul_ntt": {"mulntt": f"k_poly_mul_large<{ps}, true>"}}[op]
     return {"fwdinv": {"fwd": f"k_ntt_fwd<{ps}, false>", "inv": f"k_ntt_inv<{ps}, false>"},
