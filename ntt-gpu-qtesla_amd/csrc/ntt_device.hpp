@@ -318,11 +318,11 @@ __device__ __forceinline__ void fill_tw2(uint2 *tab)
     const uint4 *src = g_tw2img[PS][INV ? 1 : 0];
     uint4 *dst = reinterpret_cast<uint4 *>(tab);
     constexpr int ITER = (TW2_VEC4 + NT - 1) / NT;
-    uint4 v[ITER];
+    uint4 v[ITER];   // loads unconditional (clamped index): a conditionally set array went to scratch memory
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {
         const int i = threadIdx.x + k * NT;
-        if (i < TW2_VEC4) v[k] = src[i];
+        v[k] = src[i < TW2_VEC4 ? i : TW2_VEC4 - 1];
     }
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {

@@ -149,10 +149,6 @@ int dispatch(int ps, Args &&...args)
     }
 }
 
-#ifndef LARGE_XFORM_BIG
-#define LARGE_XFORM_BIG 1   // n = 4096 / 8192 poly_ntt / poly_invntt: one wave per polynomial (ntt_big.hpp)
-#endif
-
 // n = 4096 / 8192: polynomials per slot and step count, >= 2 workgroups per CU
 template <class LG>
 size_t large_ppw(size_t batch, const DevInfo &d)
@@ -173,7 +169,6 @@ template <int PS> struct LXform {
             // orders compose them with the bit-reversal kernel (2 launches)
             const uint32_t nb = (uint32_t)batch;
             const dim3 gb((uint32_t)(batch < (size_t)d.cus * 64 ? batch : (size_t)d.cus * 64)), bb(512);
-#if LARGE_XFORM_BIG
             // one wave per polynomial (ntt_big.hpp)
             using BG = Big<PS>;
             size_t ppw = batch / ((size_t)BG::WAVES * d.cus * 2);
@@ -181,14 +176,6 @@ template <int PS> struct LXform {
             const dim3 g((uint32_t)((batch + BG::WAVES * ppw - 1) / (BG::WAVES * ppw))), b(BG::NT);
             auto fwd = [&](const uint32_t *i, uint32_t *o) { hipLaunchKernelGGL(k_ntt_fwd_big<PS>, g, b, 0, s, i, o, nb, (uint32_t)ppw); };
             auto inv = [&](const uint32_t *i, uint32_t *o) { hipLaunchKernelGGL(k_ntt_inv_big<PS>, g, b, 0, s, i, o, nb, (uint32_t)ppw); };
-#else
-            // G waves per polynomial with cross-wave exchanges (ntt_large.hpp)
-            using LG = Large<PS>;
-            const size_t ppw = large_ppw<LG>(batch, d);
-            const dim3 g((uint32_t)((batch + LG::SLOTS * ppw - 1) / (LG::SLOTS * ppw))), b(LG::NT);
-            auto fwd = [&](const uint32_t *i, uint32_t *o) { hipLaunchKernelGGL(k_ntt_fwd_large<PS>, g, b, 0, s, i, o, nb, (uint32_t)ppw); };
-            auto inv = [&](const uint32_t *i, uint32_t *o) { hipLaunchKernelGGL(k_ntt_inv_large<PS>, g, b, 0, s, i, o, nb, (uint32_t)ppw); };
-#endif
             switch (k) {
             case FWD: fwd(in, out); break;
             case INV: inv(in, out); break;

@@ -1,33 +1,26 @@
-// ntt_large.hpp -- gfx950 transforms for n = 4096 and n = 8192 (param sets 3
-// and 4, p-III's prime): the multi-wave four-step dataflow of SURVEY.md 8f
-// row 3 (the reference's alternatives for other sizes are its Stockham
-// kernels, NTT.cu:1085-1153 / 1268-1337, and CT2, :667-951).  Included by
-// ntt_kernels.hip after ntt_device.hpp (it owns the __constant__ symbols).
+// ntt_large.hpp -- gfx950 fused products for n = 4096 and n = 8192 (param
+// sets 3 and 4, p-III's prime): the multi-wave four-step dataflow of SURVEY.md
+// 8f row 3 (the reference's alternatives for other sizes are its Stockham
+// kernels, NTT.cu:1085-1153 / 1268-1337, and CT2, :667-951).  The standalone
+// n = 4096 / 8192 transforms run one wave per polynomial (ntt_big.hpp); a
+// product holds two operands, which do not fit one wave's registers at
+// n = 8192, so it keeps this split.  Included by ntt_kernels.hip after
+// ntt_device.hpp (it owns the __constant__ symbols).
 //
 // One polynomial is split over G = n/2048 waves of a workgroup; wave B owns
 // sub-block B (pos = 2048 B + p').  CT DIT with merged twist, stages on pos
 // bits L-1 .. 0 (L = log2 n):
 //   * the first g = log2 G stages (pos bits L-1 .. 11) pair sub-block B with
-//     sub-block B ^ 2^(g-1-s): radix-2 stages ACROSS waves, one LDS exchange
-//     round each.  The wave holding the upper half sends t = w y (negated
-//     Shoup product), the lower one x mod 2q; each keeps one output, so no
-//     multiply is done twice;
+//     sub-block B ^ 2^(g-1-s): in registers from chunked loads plus one LDS
+//     exchange (the in-register head, LARGE_HEAD), or radix-2 stages ACROSS
+//     waves, one LDS exchange round each (cross_ct / cross_gs);
 //   * sub-block B is then a 2048-point transform whose twiddles are its own
 //     sub-tree of the n-point table, T_B[2^s + m] = psi^brv(2^s (2^g + B) + m):
 //     the n = 2048 kernel's passes (register pass, permlane32 stage, LDS
 //     transpose, register pass) with per-wave twiddle tables;
-//   * natural-order output k' of sub-block B is global index G k' + brv_g(B):
-//     the G waves of a polynomial exchange their outputs through their LDS
-//     buffers (an all-to-all, conflict-free by a per-wave rotation, see
-//     xch_pos) so that each wave stores one contiguous 2048-word block.
-//     Storing the sub-blocks directly (stride G words) wrote 1.7x / 2.5x the
-//     algorithmic bytes at n = 4096 / 8192 (partial lines, WRITE_SIZE),
-//     profiles/r02/s4/large_pmc.txt;
+//   * the product is taken in that pass-2 layout (both forwards end there,
+//     the inverse starts there), so no output all-to-all is needed;
 //   * every exchange synchronises only the G waves of its polynomial (SlotSync).
-// The inverse runs in reverse: contiguous loads scattered to the owning
-// waves through LDS (strided loads fetched 1.3x / 1.7x), the 2048-point GS
-// passes with T_B^-1 (n^-1 folded into their last stage), the g GS stages
-// across waves (LDS exchanges), contiguous stores.
 #pragma once
 #include "ntt_device.hpp"
 
@@ -500,173 +493,6 @@ __device__ __forceinline__ void large_store(uint32_t *dst, const LargeWave<LG> &
     const bool bad = w.ss.poisoned();
 #pragma unroll
     for (int j = 0; j < 32; ++j) st_out(dst + large_off<LG>(j), bad ? SYNC_SENTINEL : val(j));
-}
-
-// The standalone transforms keep their own step bodies (the same dataflow as
-// LargeWave::fwd / to_contiguous and from_contiguous / inv): written through
-// the shared helpers, the inverse's schedule spilled 13-15 VGPRs at the
-// 128-VGPR budget of 16 waves per workgroup.
-template <int PS>
-__global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_fwd_large(const uint32_t *in, uint32_t *out,
-                                                                                uint32_t npoly, uint32_t ppw)
-{
-    using LG = Large<PS>;
-    using P = typename LG::P;
-    using LT = Lane<P>;
-    constexpr int G = LG::G;
-    constexpr uint32_t N = LG::PL::N;
-    constexpr bool HEAD = LARGE_HEAD;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
-    const uint32_t first = blockIdx.x * (LG::SLOTS * ppw);
-    if (first >= npoly) return;   // whole workgroup
-    const uint32_t wave = wave_id(), B = wave % G, slot = wave / G;
-    uint32_t *const buf = lds + wave * XPOSE_WORDS;
-    // lane table (T_0's when SHARED, else T_B's image) and T_B's bit-5 table
-    const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + (LG::SHARED ? 0u : B * TW2_WORDS));
-    const uint2 *bit5 = LG::SHARED ? reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + TW2_BIT5_VEC4 * 4 + B * 64)
-                                   : tw2 + TW2_ENTRIES * 64;
-    fill_large_tw<LG, false>(lds + LG::WAVES * XPOSE_WORDS);
-    uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + LG::TAB_WORDS;
-    if (threadIdx.x <= (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;   // slot counters + poison word
-    __syncthreads();
-    SlotSync ss{ctrs + slot, ctrs + LG::SLOTS, 0};
-    const LT L;
-    const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
-#pragma unroll 1
-    for (uint32_t it = 0; it < steps; ++it) {
-        const uint32_t poly = first + it * LG::SLOTS + slot;
-        const bool valid = poly < npoly;
-        // lane offsets opaque per step: the accesses keep the scalar base +
-        // 32-bit offset form instead of loop-invariant 64-bit VGPR addresses
-        uint32_t lo = L.brl;
-        asm volatile("" : "+v"(lo));
-        uint32_t r[32];
-        if constexpr (HEAD) {
-            // in-register head (LARGE_HEAD): chunk c's words 2048 c +
-            // (2048/G) B + 64 j' + l at register (32/G) c + j', the first g
-            // stages in registers, one exchange
-            load32(r, in + (size_t)(valid ? poly : first) * N + B * (2048u / G) + lo,
-                   [](int j) { return 2048 * (j / (32 / G)) + 64 * (j % (32 / G)); });
-            head_fwd<P, G>(r, c_cross[LG::IDX][0]);
-            head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, L.lane, B, ss);
-        } else {
-        load32(r, in + (size_t)(valid ? poly : first) * N + B * 2048u + lo, [](int j) { return 64 * j; });
-        // pos bit L-1 (k = 1), then for n = 8192 pos bit 11 (k = 2 + B/2)
-        constexpr uint32_t D0 = G / 2;
-        cross_ct<P, false, G>(r, buf, lds + (wave ^ D0) * XPOSE_WORDS, L.lane, (B & D0) != 0, c_cross[LG::IDX][0][1], ss);
-        if constexpr (G == 4)
-            cross_ct<P, true, G>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0,
-                                 c_cross[LG::IDX][0][2 + (B >> 1)], ss);
-        }
-        fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), bit5 + opaque_zero());
-        lds_p1_to_p2<P>(r, buf, LT(opaque_lane()));   // addresses recomputed (see k_ntt_inv_large)
-        subtree_scale<P, LG, false>(r, B);             // T_B = c_{B,b} T_0 (c_fscale)
-        fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
-        // all-to-all through the exchange buffers: register j of lane l holds
-        // k' = brv5(j) 64 + l, global index G k' + brv_g(B); this wave then
-        // stores global words [2048 B, 2048 B + 2048), lane-contiguous runs
-#pragma unroll
-        for (int j = 0; j < 32; ++j) buf[xch_pos<G>(brv5(j) * 64 + L.lane, B)] = canon4<P>(r[j]);
-        ss.wait<G>();
-        {
-            const uint32_t bs = brv_g(L.lane % G, LG::LOGG);   // source wave of global word g (g = lane mod G)
-            const uint32_t *src = lds + (slot * G + bs) * XPOSE_WORDS;
-            const uint32_t k0 = 2048u / G * B + L.lane / G;     // k' of j = 0
-#pragma unroll
-            for (int j = 0; j < 32; ++j) r[j] = src[xch_pos<G>(k0 + 64u / G * j, bs)];
-        }
-        ss.wait<G>();   // the buffers are free for the next step's exchanges
-        if (valid) {
-            const bool bad = ss.poisoned();
-            uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
-#pragma unroll
-            for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, bad ? SYNC_SENTINEL : r[j]);
-        }
-    }
-}
-
-template <int PS>
-__global__ __launch_bounds__(Large<PS>::NT, Large<PS>::OCC) void k_ntt_inv_large(const uint32_t *in, uint32_t *out,
-                                                                                uint32_t npoly, uint32_t ppw)
-{
-    using LG = Large<PS>;
-    using P = typename LG::P;
-    using LT = Lane<P>;
-    constexpr int G = LG::G;
-    constexpr uint32_t N = LG::PL::N;
-    constexpr uint32_t NINVP = cshoup(LG::PL::NINV, P::Q);
-    constexpr bool HEAD = LARGE_HEAD;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
-    const uint32_t first = blockIdx.x * (LG::SLOTS * ppw);
-    if (first >= npoly) return;
-    const uint32_t wave = wave_id(), B = wave % G, slot = wave / G;
-    uint32_t *const buf = lds + wave * XPOSE_WORDS;
-    // lane table (T_0's when SHARED, else T_B's image) and T_B's bit-5 table
-    const uint2 *tw2 = reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + (LG::SHARED ? 0u : B * TW2_WORDS));
-    const uint2 *bit5 = LG::SHARED ? reinterpret_cast<const uint2 *>(lds + LG::WAVES * XPOSE_WORDS + TW2_BIT5_VEC4 * 4 + B * 64)
-                                   : tw2 + TW2_ENTRIES * 64;
-    fill_large_tw<LG, true>(lds + LG::WAVES * XPOSE_WORDS);
-    uint32_t *const ctrs = lds + LG::WAVES * XPOSE_WORDS + LG::TAB_WORDS;
-    if (threadIdx.x <= (uint32_t)LG::SLOTS) ctrs[threadIdx.x] = 0;   // slot counters + poison word
-    __syncthreads();
-    SlotSync ss{ctrs + slot, ctrs + LG::SLOTS, 0};
-    const LT L;
-    const uint32_t steps = (min((uint32_t)LG::SLOTS * ppw, npoly - first) + LG::SLOTS - 1) / LG::SLOTS;
-#pragma unroll 1
-    for (uint32_t it = 0; it < steps; ++it) {
-        const uint32_t poly = first + it * LG::SLOTS + slot;
-        const bool valid = poly < npoly;
-        uint32_t lo = L.brl;   // opaque per step (see k_ntt_fwd_large)
-        asm volatile("" : "+v"(lo));
-        uint32_t r[32];
-        // contiguous load of global words [2048 B, 2048 B + 2048), scattered
-        // to the owning waves: global g = G k' + brv_g(B') belongs to wave B'
-        // (the previous step's last cross_gs barrier freed the buffers)
-        load32(r, in + (size_t)(valid ? poly : first) * N + B * 2048u + lo, [](int j) { return 64 * j; });
-        {
-            const uint32_t bt = brv_g(L.lane % G, LG::LOGG);   // owner of g (g = lane mod G)
-            uint32_t *dst = lds + (slot * G + bt) * XPOSE_WORDS;
-            const uint32_t k0 = 2048u / G * B + L.lane / G;
-#pragma unroll
-            for (int j = 0; j < 32; ++j) dst[xch_pos<G>(k0 + 64u / G * j, bt)] = r[j];
-        }
-        ss.wait<G>();
-        // pass-2 register j of lane l holds sub-block index k' = brv5(j)*64 + l
-#pragma unroll
-        for (int j = 0; j < 32; ++j) r[j] = buf[xch_pos<G>(brv5(j) * 64 + L.lane, B)];
-        inv_pass2<P>(r, tw2 + opaque_zero(), L.lane);
-        subtree_scale<P, LG, true>(r, B);   // the c'_{B,b} the shared table left out (c_fscale)
-        // transpose addresses from an opaque lane: recomputed here instead of
-        // 8 loop-invariant VGPRs (which spilled at the 128-VGPR budget)
-        lds_p2_to_p1<P>(r, buf, LT(opaque_lane()));
-        inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5 + opaque_zero());
-        const uint2 last = c_lastinv[LG::IDX][0][B];
-        inv_last_stage<P, false>(r, LG::PL::NINV, NINVP, last.x, last.y);   // [0,2q), scaled by n^-1
-        if constexpr (HEAD) {
-            // mirror of the forward's head: one exchange, the last g GS
-            // stages in registers, G runs stored
-            head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, L.lane, B, ss);
-            head_inv<P, G>(r, c_cross[LG::IDX][1]);
-            if (valid) {
-                const bool bad = ss.poisoned();
-                uint32_t *dst = out + (size_t)poly * N + B * (2048u / G) + lo;
-#pragma unroll
-                for (int j = 0; j < 32; ++j)
-                    st_out(dst + 2048 * (j / (32 / G)) + 64 * (j % (32 / G)), bad ? SYNC_SENTINEL : csub<P::Q>(r[j]));
-            }
-        } else {
-        if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)
-            cross_gs<P, G>(r, buf, lds + (wave ^ 1u) * XPOSE_WORDS, L.lane, (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)], ss);
-        constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1)
-        cross_gs<P, G>(r, buf, lds + (wave ^ D0) * XPOSE_WORDS, L.lane, (B & D0) != 0, c_cross[LG::IDX][1][1], ss);
-        if (valid) {
-            const bool bad = ss.poisoned();
-            uint32_t *dst = out + (size_t)poly * N + B * 2048u + lo;
-#pragma unroll
-            for (int j = 0; j < 32; ++j) st_out(dst + 64 * j, bad ? SYNC_SENTINEL : csub<P::Q>(r[j]));
-        }
-        }
-    }
 }
 
 #ifndef MUL_PF
