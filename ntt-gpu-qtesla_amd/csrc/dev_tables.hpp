@@ -50,12 +50,13 @@ inline std::vector<uint32_t> dev_tw2_image(const ParamSet &p, const Tables &t, b
 {
     std::vector<uint32_t> o(TW2_WORDS, 0);
     auto put = [&](int slot, uint32_t k) { dev_pair(p, t, inv, kmap(k), o[2 * slot], o[2 * slot + 1]); };
+    const uint32_t lanes = logn == 11 ? 64 : 32;   // n = 1024: one entry column per 32-lane half (tw2_lanes)
     for (int e = 0; e < TW2_ENTRIES; e++) {
         const int b = e < 1 ? 4 : e < 3 ? 3 : e < 7 ? 2 : e < 15 ? 1 : 0;
         const uint32_t m = e - ((1u << (4 - b)) - 1);
-        for (uint32_t lane = 0; lane < 64; lane++) {
-            const uint32_t Lp = logn == 11 ? bitrev(lane, 6) : bitrev(lane & 31, 5);
-            put(e * 64 + lane, (1u << (logn - 1 - b)) + (Lp << (4 - b)) + m);
+        for (uint32_t lane = 0; lane < lanes; lane++) {
+            const uint32_t Lp = logn == 11 ? bitrev(lane, 6) : bitrev(lane, 5);
+            put(e * lanes + lane, (1u << (logn - 1 - b)) + (Lp << (4 - b)) + m);
         }
     }
     for (int i = 0; i < 32; i++) put(TW2_ENTRIES * 64 + i, 32u + i);

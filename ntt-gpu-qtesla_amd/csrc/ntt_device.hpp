@@ -306,6 +306,17 @@ __device__ __forceinline__ const uint2 *tw_base()
 constexpr int TW2_ENTRIES = 31;
 constexpr int TW2_WORDS = TW2_ENTRIES * 64 * 2 + 64;   // 15.5 KiB + the 32-entry bit-5 table
 constexpr int TW2_VEC4 = TW2_WORDS / 4;                // 1008 uint4
+// lanes per table entry: n = 1024 runs two polynomials per wave, one per
+// 32-lane half, whose lane twiddles are equal -- its table holds 32 lanes
+// (7.75 KiB: half the workgroup prologue, config 2's HBM traffic 1.04x ->
+// see DESIGN.md §7) and lane l reads entry column l & 31 (lanes l, l + 32
+// share an address: a broadcast, still conflict-free)
+template <class P> constexpr uint32_t tw2_lanes() { return P::LOGN == 11 ? 64u : 32u; }
+template <class P> constexpr int tw2_vec4() { return P::LOGN == 11 ? TW2_VEC4 : TW2_ENTRIES * 32 * 2 / 4; }
+template <class P> __device__ __forceinline__ uint32_t tw2_idx(int e, uint32_t lane)
+{
+    return (uint32_t)e * tw2_lanes<P>() + (lane & (tw2_lanes<P>() - 1u));
+}
 
 // Host-built images of the per-workgroup LDS twiddle table (lane-major
 // pass-2 entries + the 32-entry bit-5 table), one per (param set, direction):
@@ -315,19 +326,20 @@ __device__ uint4 g_tw2img[3][2][TW2_VEC4];
 template <int PS, bool INV, int NT>
 __device__ __forceinline__ void fill_tw2(uint2 *tab)
 {
+    constexpr int V4 = tw2_vec4<typename PSel<PS>::T>();
     const uint4 *src = g_tw2img[PS][INV ? 1 : 0];
     uint4 *dst = reinterpret_cast<uint4 *>(tab);
-    constexpr int ITER = (TW2_VEC4 + NT - 1) / NT;
+    constexpr int ITER = (V4 + NT - 1) / NT;
     uint4 v[ITER];   // loads unconditional (clamped index): a conditionally set array went to scratch memory
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {
         const int i = threadIdx.x + k * NT;
-        v[k] = src[i < TW2_VEC4 ? i : TW2_VEC4 - 1];
+        v[k] = src[i < V4 ? i : V4 - 1];
     }
 #pragma unroll
     for (int k = 0; k < ITER; ++k) {
         const int i = threadIdx.x + k * NT;
-        if (i < TW2_VEC4) dst[i] = v[k];
+        if (i < V4) dst[i] = v[k];
     }
 }
 
@@ -476,7 +488,7 @@ __device__ __forceinline__ void fwd_pass2_lz(uint32_t (&r)[32], const uint2 *tab
         for (int j = 0; j < 32; ++j) {
             if ((j & hh) == 0) {
                 const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
-                const uint2 w = tab[e * 64 + lane];
+                const uint2 w = tab[tw2_idx<P>(e, lane)];
                 const bool xs = b < 4 && (j & (2 * hh)) != 0;          // x came out S from stage b+1
                 const bool yos = b == BMIN || ((j + hh) & (hh >> 1)) == 0;
                 if (xs) {
@@ -503,7 +515,7 @@ __device__ __forceinline__ void fwd_pass2(uint32_t (&r)[32], const uint2 *tab, u
         for (int j = 0; j < 32; ++j) {
             if ((j & hh) == 0) {
                 const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
-                const uint2 w = tab[e * 64 + lane];
+                const uint2 w = tab[tw2_idx<P>(e, lane)];
                 ct_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
             }
         }
@@ -523,7 +535,7 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
         for (int j = 0; j < 32; ++j) {
             if ((j & hh) == 0) {
                 const int e = (1 << (4 - b)) - 1 + (j >> (b + 1));
-                const uint2 w = tab[e * 64 + lane];
+                const uint2 w = tab[tw2_idx<P>(e, lane)];
                 if (WIDE0 && b == BMIN) {
                     const uint32_t x = r[j], y = r[j + hh], sm = x + y;   // [0, 6q)
                     r[j] = umin(umin(sm, sm - P::Q2), sm - 2 * P::Q2);
@@ -626,7 +638,7 @@ struct BaseMul {
     {
 #pragma unroll
         for (int gp = 0; gp < 16 / D; ++gp) {
-            const uint2 w = tab[(E0 + gp) * 64 + lane];   // (-w mod 2^32, w')
+            const uint2 w = tab[tw2_idx<P>(E0 + gp, lane)];   // (-w mod 2^32, w')
             // -(w R mod q) in (-2q, 0] (negated Shoup product of the constant R)
             const uint32_t tn = madlo32(__umulhi(P::R, w.y), P::Q, P::R * w.x);
             const uint32_t zr[2] = {umin(0u - tn, (0u - P::Q) - tn),   // +w: w R mod q in [0, q]
@@ -671,7 +683,7 @@ struct BaseMul {
 #endif
 #pragma unroll
         for (int g = 0; g < 32 / D; ++g) {
-            const uint2 w = tab[(E0 + (g >> 1)) * 64 + lane];   // (-w mod 2^32, w')
+            const uint2 w = tab[tw2_idx<P>(E0 + (g >> 1), lane)];   // (-w mod 2^32, w')
             uint32_t a[D], b[D], bt[D];
 #pragma unroll
             for (int i = 0; i < D; ++i) {

@@ -321,9 +321,12 @@ __device__ __forceinline__ void subtree_scale(uint32_t (&r)[32], uint32_t B)
 {
     if constexpr (!LG::SHARED) return;
     if (B == 0) return;   // wave-uniform
-    const uint2 *f = c_fscale[LG::IDX][INV ? 1 : 0][B] + opaque_zero();
+    const uint2 *f;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) r[j] = shoup_mul<P::Q>(r[j], f[j].x, f[j].y);
+    for (int j = 0; j < 32; ++j) {
+        if ((j & 7) == 0) f = c_fscale[LG::IDX][INV ? 1 : 0][B] + opaque_zero();   // 8 pairs in SGPRs at a time
+        r[j] = shoup_mul<P::Q>(r[j], f[j].x, f[j].y);
+    }
 }
 
 // Per-wave state of the large-n kernels: the wave's sub-block B and slot,
@@ -358,9 +361,34 @@ struct LargeWave {
     template <int D>
     __device__ __forceinline__ void table(uint32_t *t)
     {
+        table_ptrs<D>(t);
+        fill_large_tw<LG, D == 1>(t);
+    }
+    template <int D>
+    __device__ __forceinline__ void table_ptrs(uint32_t *t)
+    {
         tw2[D] = reinterpret_cast<const uint2 *>(t + (LG::SHARED ? 0u : B * TW2_WORDS));
         bit5[D] = LG::SHARED ? reinterpret_cast<const uint2 *>(t + TW2_BIT5_VEC4 * 4 + B * 64) : tw2[D] + TW2_ENTRIES * 64;
-        fill_large_tw<LG, D == 1>(t);
+    }
+    // Re-derive the wave-uniform state from an opaque wave index at the top of
+    // every step: otherwise every address, table pointer and branch mask
+    // derived from it is hoisted out of the step loop and held for the whole
+    // kernel (33 spilled SGPRs in the n = 8192 b-hat product)
+    template <int D0, int D1>
+    __device__ __forceinline__ void refresh()
+    {
+        uint32_t wv = wave_id();
+        asm volatile("" : "+s"(wv));
+        wave = wv;
+        B = wv % LG::G;
+        slot = wv / LG::G;
+        buf = lds + wv * XPOSE_WORDS;
+        uint32_t *tab = lds + LG::WAVES * XPOSE_WORDS;
+        if constexpr (D0 == 0) table_ptrs<0>(tab);
+        if constexpr (D1 == 1) table_ptrs<1>(tab + (D0 == 0 ? LG::TAB_WORDS : 0));
+        uint32_t *const ctrs = tab + LG::NTAB * LG::TAB_WORDS;
+        ss.ctr = ctrs + slot;
+        ss.poison = ctrs + LG::SLOTS;
     }
     __device__ __forceinline__ const uint32_t *partner(uint32_t d) const { return lds + (wave ^ d) * XPOSE_WORDS; }
 
@@ -531,6 +559,7 @@ void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_
     LargeWave<LG> w;
     w.template init<0, 1>(lds);
     auto step = [&](size_t pbase, bool valid) {
+        w.template refresh<0, 1>();
         uint32_t ra[32], rb[32];
         // this wave's words: the forward's input layout (large_off), b-hat
         // contiguous (the scatter of from_contiguous)
