@@ -70,7 +70,7 @@ __constant__ uint2 c_bigtw[LARGE_NPS][2][BIG_RMAX];
 // the R bit-5 pairs, [set][fwd/inv]
 __device__ uint4 g_bigimg[LARGE_NPS][2][BIG_IMG_VEC4_MAX];
 
-template <int PS>
+template <int PS, int WV = 0>
 struct Big {
     using PL = typename PSel<PS>::T;   // the n-point set
     using P = PS2;                     // same prime; butterflies only use Q
@@ -82,7 +82,7 @@ struct Big {
     static constexpr int NC = L - 11;
     static constexpr int CH = 1 << NC;
     static constexpr int IDX = PS - LARGE_PS0;
-    static constexpr int WAVES = L == 12 ? 16 : BIG_WAVES_8192;
+    static constexpr int WAVES = WV ? WV : L == 12 ? 16 : BIG_WAVES_8192;
     static constexpr int NT = WAVES * 64;
     static constexpr int OCC = (WAVES + 3) / 4;                   // waves per SIMD
     static constexpr int LANE_PAIRS = TW2_ENTRIES * 64 * CH;      // lane table
@@ -194,6 +194,130 @@ __device__ __forceinline__ void big_fwd_bit5(uint32_t (&r)[BG::R], const uint2 *
     });
 }
 
+// Forward from layout A (registers r, inputs < 2q): pass 1, the bit-5 stage
+// and, chunk by chunk, the transpose to layout B and the pass-2 stages on pos
+// 4 .. BMIN (BMIN > 0 stops short, the products' incomplete domain);
+// sink(C, v) takes chunk C's 32 B-layout registers, in [0, 4q).
+template <class BG, int BMIN, class Sink>
+__device__ __forceinline__ void big_fwd(uint32_t (&r)[BG::R], uint32_t *buf, const uint2 *tab, uint32_t h, uint32_t lane,
+                                        Sink &&sink)
+{
+    using P = typename BG::P;
+    big_fwd_pass1<BG>(r);
+    big_fwd_bit5<BG>(r, tab + BG::LANE_PAIRS + opaque_zero(), h);
+    sfor<BG::CH>([&](auto C) {
+        constexpr int c = C;
+        // transpose addresses recomputed per chunk from an opaque lane
+        // (not 16 loop-invariant address VGPRs)
+        const uint32_t wb = big_wbase(opaque_lane());
+        const Lane<P> LB(opaque_lane());   // the n = 2048 b128 read side (Lp = brv6(lane))
+        sfor<32>([&](auto T) { buf[big_waddr(wb, T)] = r[BG::creg(c, T)]; });
+        compiler_fence();
+        uint32_t v[32];
+        sfor<8>([&](auto Q) {
+            const uint4 x = *reinterpret_cast<const uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm));
+            v[4 * Q + 0] = x.x;
+            v[4 * Q + 1] = x.y;
+            v[4 * Q + 2] = x.z;
+            v[4 * Q + 3] = x.w;
+        });
+        compiler_fence();
+        fwd_pass2<P, BMIN>(v, tab + TW2_ENTRIES * 64 * c + opaque_zero(), lane);
+        sink(C, v);
+    });
+}
+
+// Inverse to layout A, stored at dst (the polynomial's first word): chunk by
+// chunk source(C, v) gives the 32 B-layout registers (inputs of the stage on
+// pos BMIN, WIDE0: inv_pass2's wide first stage), GS pass 2 and the transpose
+// back; then the GS bit-5 stage and swap, the GS stages on pos 6 .. L-2 and
+// the last one scaled by S0 (x + y) and S1 (x - y), canonical.
+template <class BG, int BMIN, bool WIDE0, uint32_t S0, uint32_t S1V, class Source>
+__device__ __forceinline__ void big_inv(uint32_t (&r)[BG::R], uint32_t *buf, const uint2 *tab, uint32_t h, uint32_t lane,
+                                        Source &&source, uint32_t *dpoly)
+{
+    using P = typename BG::P;
+    constexpr int M = BG::M, H = BG::H;
+    sfor<BG::CH>([&](auto C) {
+        constexpr int c = C;
+        const uint32_t wb = big_wbase(opaque_lane());   // per chunk (see big_fwd)
+        const Lane<P> LB(opaque_lane());
+        uint32_t v[32];
+        source(C, v);
+        inv_pass2<P, BMIN, WIDE0>(v, tab + TW2_ENTRIES * 64 * c + opaque_zero(), lane);
+        sfor<8>([&](auto Q) {
+            *reinterpret_cast<uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm)) =
+                make_uint4(v[4 * Q + 0], v[4 * Q + 1], v[4 * Q + 2], v[4 * Q + 3]);
+        });
+        compiler_fence();
+        sfor<32>([&](auto T) { r[BG::creg(c, T)] = buf[big_waddr(wb, T)]; });
+        compiler_fence();
+    });
+    // bit-5 stage: GS with the lane-half twiddle, then swap back
+    const uint2 *sw = tab + BG::LANE_PAIRS + opaque_zero();
+    sfor<H>([&](auto Mi) {
+        constexpr int m = Mi;
+        const uint2 w = sw[m + H * h];
+        gs_bfly<P::Q>(r[m], r[m + H], w.x, w.y);
+        const auto pr = __builtin_amdgcn_permlane32_swap(r[m], r[m + H], false, false);
+        r[m] = pr[0];
+        r[m + H] = pr[1];
+    });
+    // GS stages on pos 6 .. L-2 (register bits 0 .. M-2), uniform twiddles
+    sfor<M - 1>([&](auto JB) {
+        constexpr int jb = JB, hh = 1 << jb, s = M - 1 - jb;
+        sfor<BG::R / 32>([&](auto B) {
+            const uint2 *tw = big_tw<BG>(true);   // <= 16 pairs in SGPRs at a time
+            sfor<32>([&](auto J) {
+                constexpr int j = 32 * B + J;
+                if constexpr ((j & hh) == 0) {
+                    const uint2 w = tw[(1 << s) + (j >> (jb + 1))];
+                    gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
+                }
+            });
+        });
+    });
+    // last stage (pos L-1): x' = (x + y) S0, y' = (x - y) S1 (S1 = S0 psi^-brv(1))
+    constexpr uint32_t S0P = cshoup(S0, P::Q);
+    constexpr TwPair S1 = csigned_tw(S1V, P::Q);
+    uint32_t lo = lane;
+    asm volatile("" : "+v"(lo));
+    uint32_t *const dst = dpoly + lo;
+    sfor<H>([&](auto J) {
+        constexpr int j = J;
+        const uint32_t x = r[j], y = r[j + H];
+        st_out(dst + 64u * j, csub<P::Q>(shoup_mul<P::Q>(x + y, S0, S0P)));
+        st_out(dst + 64u * (j + H), csub<P::Q>(sshoup_mul<P::Q>(x - y, S1.x, S1.y)));
+    });
+}
+
+// register pins: the values are taken as redefined here, so the scheduler
+// keeps the phases on either side apart (register pressure)
+template <int NR>
+__device__ __forceinline__ void pin(uint32_t (&r)[NR])
+{
+#pragma unroll
+    for (int j = 0; j < NR; ++j) asm volatile("" : "+v"(r[j]));
+}
+
+// layout A loads: natural order, 256-B runs
+template <class BG>
+__device__ __forceinline__ void big_load_a(uint32_t (&r)[BG::R], const uint32_t *src, uint32_t lane)
+{
+    uint32_t lo = lane;
+    asm volatile("" : "+v"(lo));
+    load32n<BG::R>(r, src + lo, [](int j) { return 64u * (uint32_t)j; });
+}
+
+// layout B of every chunk (the forward's store order), in the chunk's register slots j(c, j')
+template <class BG>
+__device__ __forceinline__ void big_load_b(uint32_t (&r)[BG::R], const uint32_t *src, uint32_t lane)
+{
+    uint32_t lo = lane;
+    asm volatile("" : "+v"(lo));
+    sfor<BG::CH>([&](auto C) { sfor<32>([&](auto JP) { r[BG::creg(C, JP)] = ld_in(src + lo + BG::boff(C, JP)); }); });
+}
+
 template <int PS>
 __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_fwd_big(const uint32_t *in, uint32_t *out, uint32_t npoly,
                                                                         uint32_t ppw)
@@ -210,36 +334,15 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_fwd_big(const
     const uint32_t lane = threadIdx.x & 63, h = lane >> 5;
     uint32_t *const buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint2 *const tab = reinterpret_cast<const uint2 *>(tabw);
-    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {   // layout A: natural, 256-B runs
-        uint32_t lo = lane;
-        asm volatile("" : "+v"(lo));
-        load32n<BG::R>(r, in + (size_t)u * N + lo, [](int j) { return 64u * (uint32_t)j; });
-    };
+    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) { big_load_a<BG>(r, in + (size_t)u * N, lane); };
     auto process = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
-        big_fwd_pass1<BG>(r);
-        big_fwd_bit5<BG>(r, tab + BG::LANE_PAIRS + opaque_zero(), h);
         uint32_t lo = lane;   // opaque per unit: scalar base + 32-bit lane offset stores
         asm volatile("" : "+v"(lo));
         uint32_t *const dst = out + (size_t)u * N + lo;
-        sfor<BG::CH>([&](auto C) {
-            constexpr int c = C;
-            // transpose addresses recomputed per chunk from an opaque lane
-            // (not 16 loop-invariant address VGPRs)
-            const uint32_t wb = big_wbase(opaque_lane());
-            const Lane<P> LB(opaque_lane());   // the n = 2048 b128 read side (Lp = brv6(lane))
-            sfor<32>([&](auto T) { buf[big_waddr(wb, T)] = r[BG::creg(c, T)]; });
-            compiler_fence();
-            uint32_t v[32];
-            sfor<8>([&](auto Q) {
-                const uint4 x = *reinterpret_cast<const uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm));
-                v[4 * Q + 0] = x.x;
-                v[4 * Q + 1] = x.y;
-                v[4 * Q + 2] = x.z;
-                v[4 * Q + 3] = x.w;
-            });
-            compiler_fence();
-            fwd_pass2<P>(v, tab + TW2_ENTRIES * 64 * c + opaque_zero(), lane);
-            sfor<32>([&](auto JP) { st_out(dst + BG::boff(c, JP), canon4<P>(v[JP])); });
+        // every store is a lane-contiguous 256-B run, chunk by chunk (the
+        // stores of chunk c overlap chunk c+1's transpose and arithmetic)
+        big_fwd<BG, 0>(r, buf, tab, h, lane, [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {
+            sfor<32>([&](auto JP) { st_out(dst + BG::boff(C, JP), canon4<P>(v[JP])); });
         });
     };
     big_loop<BG>(npoly, ppw, prologue, load, process);
@@ -250,9 +353,7 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const
                                                                         uint32_t ppw)
 {
     using BG = Big<PS>;
-    using P = typename BG::P;
     constexpr uint32_t N = BG::PL::N;
-    constexpr int M = BG::M, H = BG::H;
     __shared__ __attribute__((aligned(16))) uint32_t lds[BG::LDS_WORDS];
     uint32_t *const tabw = lds + BG::WAVES * XPOSE_WORDS;
     auto prologue = [&]() {
@@ -262,65 +363,106 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const
     const uint32_t lane = threadIdx.x & 63, h = lane >> 5;
     uint32_t *const buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint2 *const tab = reinterpret_cast<const uint2 *>(tabw);
-    // layout B of every chunk, in the chunk's register slots j(c, j')
-    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
-        uint32_t lo = lane;
-        asm volatile("" : "+v"(lo));
-        const uint32_t *src = in + (size_t)u * N + lo;
-        sfor<BG::CH>([&](auto C) { sfor<32>([&](auto JP) { r[BG::creg(C, JP)] = ld_in(src + BG::boff(C, JP)); }); });
-    };
+    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) { big_load_b<BG>(r, in + (size_t)u * N, lane); };
     auto process = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
-        sfor<BG::CH>([&](auto C) {
-            constexpr int c = C;
-            const uint32_t wb = big_wbase(opaque_lane());   // per chunk (see the forward)
-            const Lane<P> LB(opaque_lane());
-            uint32_t v[32];
-            sfor<32>([&](auto JP) { v[JP] = r[BG::creg(c, JP)]; });
-            inv_pass2<P>(v, tab + TW2_ENTRIES * 64 * c + opaque_zero(), lane);
-            sfor<8>([&](auto Q) {
-                *reinterpret_cast<uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm)) =
-                    make_uint4(v[4 * Q + 0], v[4 * Q + 1], v[4 * Q + 2], v[4 * Q + 3]);
-            });
-            compiler_fence();
-            sfor<32>([&](auto T) { r[BG::creg(c, T)] = buf[big_waddr(wb, T)]; });
-            compiler_fence();
-        });
-        // bit-5 stage: GS with the lane-half twiddle, then swap back
-        const uint2 *sw = tab + BG::LANE_PAIRS + opaque_zero();
-        sfor<H>([&](auto Mi) {
-            constexpr int m = Mi;
-            const uint2 w = sw[m + H * h];
-            gs_bfly<P::Q>(r[m], r[m + H], w.x, w.y);
-            const auto pr = __builtin_amdgcn_permlane32_swap(r[m], r[m + H], false, false);
-            r[m] = pr[0];
-            r[m + H] = pr[1];
-        });
-        // GS stages on pos 6 .. L-2 (register bits 0 .. M-2), uniform twiddles
-        sfor<M - 1>([&](auto JB) {
-            constexpr int jb = JB, hh = 1 << jb, s = M - 1 - jb;
-            sfor<BG::R / 32>([&](auto B) {
-                const uint2 *tw = big_tw<BG>(true);   // <= 16 pairs in SGPRs at a time
-                sfor<32>([&](auto J) {
-                    constexpr int j = 32 * B + J;
-                    if constexpr ((j & hh) == 0) {
-                        const uint2 w = tw[(1 << s) + (j >> (jb + 1))];
-                        gs_bfly<P::Q>(r[j], r[j + hh], w.x, w.y);
-                    }
-                });
-            });
-        });
-        // last stage (pos L-1) with n^-1: x' = (x + y) n^-1, y' = (x - y) n^-1 psi^-brv(1)
-        constexpr uint32_t S0 = BG::PL::NINV, S0P = cshoup(S0, P::Q);
-        constexpr TwPair S1 = csigned_tw(BG::PL::C1, P::Q);
-        uint32_t lo = lane;
-        asm volatile("" : "+v"(lo));
-        uint32_t *const dst = out + (size_t)u * N + lo;
-        sfor<H>([&](auto J) {
-            constexpr int j = J;
-            const uint32_t x = r[j], y = r[j + H];
-            st_out(dst + 64u * j, csub<P::Q>(shoup_mul<P::Q>(x + y, S0, S0P)));
-            st_out(dst + 64u * (j + H), csub<P::Q>(sshoup_mul<P::Q>(x - y, S1.x, S1.y)));
-        });
+        big_inv<BG, 0, false, BG::PL::NINV, BG::PL::C1>(
+            r, buf, tab, h, lane,
+            [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) { sfor<32>([&](auto JP) { v[JP] = r[BG::creg(C, JP)]; }); },
+            out + (size_t)u * N);
+    };
+    big_loop<BG>(npoly, ppw, prologue, load, process);
+}
+
+// Fused products with one wave per polynomial (n = 4096; n = 8192's operands
+// do not fit one wave's registers and stay on k_poly_mul_large):
+//   poly_mul (BHAT false): FWD(a) and FWD(b) down to residues mod x^8 -+ zeta
+//     (big_fwd stopping at pos bit LOGR, layout B kept in registers), the
+//     residue products chunk by chunk (BaseMul, the n = 2048 product's), and
+//     the inverse from pos bit LOGR; (n/8)^-1 and the REDC's 2^32 in the last
+//     stage's constants.
+//   poly_mul_ntt (BHAT true): b-hat = poly_ntt(b) read in the forward's
+//     store order (layout B), the complete FWD(a), one Montgomery product per
+//     coefficient, the inverse with n^-1 2^32.
+// a, b and c may alias: a wave loads its polynomial's a and b before it
+// stores any c.  BIG_MUL_WAVES transpose buffers (8 KiB each) and both
+// directions' tables (2 x 31.5 KiB) in LDS; the register phases are pinned
+// apart (pin), without which the scheduler interleaves a's forward with b's.
+// Measured per 2^18 products (profiles/r04/f/ab_m4096.log): poly_mul 5.75 ms
+// (k_poly_mul_large) -> 4.82 (12 waves) -> 4.49 (8 waves); poly_mul_ntt
+// 4.20 -> 3.90 -> 3.67.
+#ifndef BIG_MUL_WAVES
+#define BIG_MUL_WAVES 8   // 2 per SIMD, 0 spills (12 waves = 3 per SIMD: 27 VGPRs spilled, 7 % slower)
+#endif
+#ifndef BIG_MUL_PF
+// b's loads issued before a's forward: poly_mul_ntt 3.64 -> 3.55 ms, poly_mul
+// 4.24 -> 4.39 (profiles/r04/g/ab_m4096.log), so b-hat only
+#define BIG_MUL_PF BHAT
+#endif
+#ifndef BIG_MUL
+#define BIG_MUL 1   // 0: n = 4096 products on k_poly_mul_large (A/B)
+#endif
+template <int PS, bool BHAT>
+__global__ __launch_bounds__((Big<PS, BIG_MUL_WAVES>::NT), (Big<PS, BIG_MUL_WAVES>::OCC)) void k_poly_mul_big(
+    const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
+{
+    using BG = Big<PS, BIG_MUL_WAVES>;
+    using P = typename BG::P;
+    using PL = typename BG::PL;
+    constexpr int LOGR = mul_logr<2>();   // p-III's prime: the n = 2048 product's residues
+    using BM = BaseMul<P, LOGR>;
+    constexpr uint32_t N = PL::N;
+    static_assert(BG::WAVES * XPOSE_WORDS + 2 * BG::IMG_WORDS <= 160 * 256, "one workgroup per CU");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BG::WAVES * XPOSE_WORDS + 2 * BG::IMG_WORDS];
+    uint32_t *const tabfw = lds + BG::WAVES * XPOSE_WORDS, *const tabiw = tabfw + BG::IMG_WORDS;
+    auto prologue = [&]() {
+        fill_big_tw<BG, false>(tabfw);
+        fill_big_tw<BG, true>(tabiw);
+        __syncthreads();
+    };
+    const uint32_t lane = threadIdx.x & 63, h = lane >> 5;
+    uint32_t *const buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
+    const uint2 *const ftab = reinterpret_cast<const uint2 *>(tabfw);
+    const uint2 *const itab = reinterpret_cast<const uint2 *>(tabiw);
+    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) { big_load_a<BG>(r, a + (size_t)u * N, lane); };
+    auto process = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
+        const size_t base = (size_t)u * N;
+        auto keep = [&](uint32_t (&x)[BG::R]) __attribute__((always_inline)) {
+            return [&x](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) { sfor<32>([&](auto JP) { x[BG::creg(C, JP)] = v[JP]; }); };
+        };
+        uint32_t rb[BG::R];
+        if constexpr (!BHAT) {
+            if constexpr (BIG_MUL_PF) big_load_a<BG>(rb, b + base, lane);
+            big_fwd<BG, LOGR>(r, buf, ftab, h, lane, keep(r));
+            pin(r);   // phase boundary: nothing of b's forward moves above it
+            if constexpr (!BIG_MUL_PF) big_load_a<BG>(rb, b + base, lane);   // 64 fewer live VGPRs through a's forward
+            big_fwd<BG, LOGR>(rb, buf, ftab, h, lane, keep(rb));
+            pin(rb);
+            big_inv<BG, LOGR, BM::WIDE, PL::template ninv_r<LOGR>(), PL::template c1_r<LOGR>()>(
+                r, buf, itab, h, lane,
+                [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {
+                    constexpr int cc = C;
+                    uint32_t vb[32];
+                    sfor<32>([&](auto JP) {
+                        v[JP] = r[BG::creg(cc, JP)];
+                        vb[JP] = rb[BG::creg(cc, JP)];
+                    });
+                    BM::run(v, vb, ftab + TW2_ENTRIES * 64 * cc + opaque_zero(), lane);
+                },
+                c + base);
+        } else {
+            if constexpr (BIG_MUL_PF) big_load_b<BG>(rb, b + base, lane);
+            big_fwd<BG, 0>(r, buf, ftab, h, lane, keep(r));
+            pin(r);
+            if constexpr (!BIG_MUL_PF) big_load_b<BG>(rb, b + base, lane);   // b-hat in the forward's store order
+            big_inv<BG, 0, false, PL::NINV_R, PL::C1_R>(
+                r, buf, itab, h, lane,
+                [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {
+                    sfor<32>([&](auto JP) {
+                        v[JP] = mont_mul<P>(csub<P::Q2>(r[BG::creg(C, JP)]), csub<P::Q2>(rb[BG::creg(C, JP)]));
+                    });
+                },
+                c + base);
+        }
     };
     big_loop<BG>(npoly, ppw, prologue, load, process);
 }

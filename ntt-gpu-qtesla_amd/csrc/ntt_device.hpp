@@ -1058,7 +1058,10 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
         constexpr bool LZ = !BHAT && MUL_LAZYBIAS;   // typed forwards (fwd_pass1_lz)
         if constexpr (LZ) fwd_pass1_lz<P>(ra, L.h, tw_base<PS, false>(), ftw2 + TW2_ENTRIES * 64 + opaque_zero());
         else fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
-        lds_p1_to_p2<P>(ra, buf, (BHAT || MUL_HOIST) ? L : LT(opaque_lane()));
+        // b-hat product: n = 2048 keeps the hoisted addresses, n = 1024 (32-lane
+        // twiddle table) recomputes them (hoisted: 22 spilled VGPRs)
+        constexpr bool HOIST = BHAT ? P::LOGN == 11 : MUL_HOIST;
+        lds_p1_to_p2<P>(ra, buf, HOIST ? L : LT(opaque_lane()));
         if constexpr (LZ) fwd_pass2_lz<P, mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
         else fwd_pass2<P, BHAT ? 0 : mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
         // b-hat is in natural order: register j of the pass-2 layout holds
@@ -1091,7 +1094,7 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
 #pragma unroll
             for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(csub<P::Q2>(ra[j]), csub<P::Q2>(rb[j]));   // b-hat < 2q
             inv_pass2<P>(ra, itw2 + opaque_zero(), L.lane);
-            lds_p2_to_p1<P>(ra, buf, L);
+            lds_p2_to_p1<P>(ra, buf, HOIST ? L : LT(opaque_lane()));
             inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
         }
     }

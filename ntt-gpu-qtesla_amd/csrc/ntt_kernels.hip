@@ -216,7 +216,16 @@ template <int PS> struct LMul {
     static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s, bool bhat,
                    const DevInfo &d)
     {
-        if constexpr (PS >= LARGE_PS0) {
+        if constexpr (PS >= LARGE_PS0 && BIG_MUL && PSel<PS>::T::N == 4096) {
+            // one wave per product (ntt_big.hpp)
+            using BG = Big<PS, BIG_MUL_WAVES>;
+            size_t ppw = batch / ((size_t)BG::WAVES * d.cus * 2);
+            ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
+            const dim3 g((uint32_t)((batch + BG::WAVES * ppw - 1) / (BG::WAVES * ppw))), blk(BG::NT);
+            if (bhat) hipLaunchKernelGGL((k_poly_mul_big<PS, true>), g, blk, 0, s, a, b, c, (uint32_t)batch, (uint32_t)ppw);
+            else hipLaunchKernelGGL((k_poly_mul_big<PS, false>), g, blk, 0, s, a, b, c, (uint32_t)batch, (uint32_t)ppw);
+            return finish_launch();
+        } else if constexpr (PS >= LARGE_PS0) {
             if (bhat) launch_mul_large<PS, true>(a, b, c, batch, s, d);
             else launch_mul_large<PS, false>(a, b, c, batch, s, d);
             return finish_launch();

@@ -552,7 +552,7 @@ void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_
 {
     using LG = Large<PS, mul_large_waves<PS, BHAT>()>;
     using P = typename LG::P;
-    constexpr bool PF = MUL_PF;
+    constexpr bool PF = MUL_PF && !(LG::G == 4 && !BHAT);
     __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
     const uint32_t first = blockIdx.x * (LG::SLOTS * ppw);
     if (first >= npoly) return;
@@ -571,6 +571,8 @@ void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_
         load32(ra, a + base + opaque_lane(), [](int j) { return large_off<LG>(j); });
         if (PF) load32(rb, b + bbase + opaque_lane(), boff);
         w.fwd(ra);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) asm volatile("" : "+v"(ra[j]));   // phase boundary (register pressure)
         if (!PF) load32(rb, b + bbase + opaque_lane(), boff);
         if constexpr (BHAT) {   // b-hat < 2q
             // the scatter writes the partners' buffers: their forward

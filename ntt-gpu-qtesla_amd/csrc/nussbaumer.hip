@@ -144,9 +144,10 @@ struct Ring<NTT_RING_M32, P> {
     static constexpr int RB = 0, IN = 0, HR = 1 << 20;
     static __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b)
     {
-        uint32_t t;
-        const bool c = __builtin_add_overflow(a, b, &t);
-        return t + (uint32_t)c;
+        // 33-bit sum in a 64-bit VALU add (no carry in an SGPR pair), then
+        // the end-around carry: lo + hi cannot wrap (hi = 1 -> lo <= 2^32 - 2)
+        const uint64_t t = (uint64_t)a + b;
+        return (uint32_t)t + (uint32_t)(t >> 32);
     }
     static __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b)
     {

@@ -70,6 +70,28 @@ K32(v_add_co_u32, "v_add_co_u32 %0, vcc, %0, %1")
 K32(v_addc_co_u32, "v_addc_co_u32 %0, vcc, %0, %1, vcc")
 K32(v_cmp_lt_u32, "v_cmp_lt_u32 vcc, %0, %1")
 K32(v_bfe_u32, "v_bfe_u32 %0, %0, 1, 7")
+// v_cndmask with its condition in an SGPR pair that nothing in the loop
+// writes (the K32 form above clobbers vcc in every asm statement)
+#define KSEL(NAME, ASM)                                                                   \
+    __global__ __launch_bounds__(256) void k_##NAME(unsigned *out, unsigned seed, int iters) \
+    {                                                                                     \
+        unsigned a[8];                                                                    \
+        for (int k = 0; k < 8; k++) a[k] = (threadIdx.x ^ seed) + k;                      \
+        const unsigned b = seed | 1;                                                      \
+        unsigned long long m;                                                             \
+        asm volatile("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(m) : "v"(a[0]), "v"(b));         \
+        for (int i = 0; i < iters; i++) {                                                 \
+            _Pragma("unroll") for (int u = 0; u < 4; u++)                                 \
+            _Pragma("unroll") for (int k = 0; k < 8; k++)                                 \
+                asm volatile(ASM : "+v"(a[k]) : "v"(b), "s"(m));                          \
+        }                                                                                 \
+        unsigned r = 0;                                                                   \
+        for (int k = 0; k < 8; k++) r ^= a[k];                                            \
+        out[blockIdx.x * 256 + threadIdx.x] = r;                                          \
+    }
+KSEL(v_cndmask_b32_sgpr, "v_cndmask_b32_e64 %0, %0, %1, %2")
+KSEL(v_cndmask_b32_sgpr_neg, "v_cndmask_b32_e64 %0, %0, -%1, %2")
+
 K64(v_mad_u64_u32, "v_mad_u64_u32 %0, vcc, %1, %1, %0")
 K64(v_mad_i64_i32, "v_mad_i64_i32 %0, vcc, %1, %1, %0")
 K64(v_lshl_add_u64, "v_lshl_add_u64 %0, %0, 1, %0")
@@ -111,7 +133,7 @@ int main(int argc, char **argv)
               E(v_add3_u32), E(v_xor_b32), E(v_and_b32), E(v_or_b32), E(v_mov_b32), E(v_lshlrev_b32),
               E(v_lshrrev_b32), E(v_ashrrev_i32), E(v_bitop3_b32), E(v_lshl_or_b32), E(v_lshl_add_u32),
               E(v_and_or_b32), E(v_mul_lo_u32), E(v_mul_hi_u32), E(v_mul_hi_i32), E(v_mul_u32_u24),
-              E(v_cndmask_b32), E(v_add_co_u32), E(v_addc_co_u32), E(v_cmp_lt_u32), E(v_bfe_u32),
+              E(v_cndmask_b32), E(v_cndmask_b32_sgpr), E(v_cndmask_b32_sgpr_neg), E(v_add_co_u32), E(v_addc_co_u32), E(v_cmp_lt_u32), E(v_bfe_u32),
               E(v_mad_u64_u32), E(v_mad_i64_i32), E(v_lshl_add_u64), E(v_lshlrev_b64), E(v_mov_b64),
               {"v_permlane32_swap_b32", k_v_permlane32_swap_b32, 16}};
     hipEvent_t e0, e1;
