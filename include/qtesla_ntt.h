@@ -195,10 +195,10 @@ int ntt_last_hip_error(void);
 const char *ntt_strerror(int code);
 
 /* Diagnostic: on the current device, the number of bounded waits of the
- * n = 4096 / 8192 kernels' per-polynomial barriers that expired since the
- * library was loaded (synchronises the device).  Always 0 unless the
- * hardware schedule broke the barrier; a launch that raised it produced
- * invalid output. */
+ * n = 8192 fused products' per-polynomial barriers that expired since the
+ * library was loaded (synchronises the device; every other kernel runs one
+ * wave per polynomial and has none).  Always 0 unless the hardware schedule
+ * broke the barrier; a launch that raised it produced invalid output. */
 int ntt_sync_expiries(uint32_t *count);
 
 /* Library / kernel description for reports, ending in "src=<16 hex>" (a hash

@@ -79,6 +79,7 @@ for step in "$@"; do
         # VALU roofline inputs (tools/valu_summary.py): per-opcode issue cost, and
         # SQ_INSTS_VALU + GRBM_GUI_ACTIVE per launch of a config's kernel
         valucost) run valucost 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU --output-format csv -d gpurun_out/valucost -o run -- ./ntt-gpu-qtesla_amd/bin/valu_cost 16384 ;;
+        valum_*) n=${step#valum_}; b=$((1073741824 / n)); run valum_$n 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valum_$n -o run -- python3 bench.py --op polymul --param p-III-$n --batch $b --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
         valu_c*) c=${step#valu_c}; run valu_c$c 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valu_c$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac

@@ -32,11 +32,13 @@ def load(path):
 
 
 def kernel_patterns(op, ps, ring):
-    if ps >= 3:   # n = 4096 / 8192: the multi-wave four-step kernels
+    if ps >= 3:   # n = 4096 / 8192: wave-per-polynomial transforms (and n = 4096 products),
+        # the n = 8192 products on the multi-wave four-step kernel
+        mk = "k_poly_mul_big" if ps == 3 else "k_poly_mul_large"
         return {"fwdinv": {"fwd": f"k_ntt_fwd_big<{ps}>", "inv": f"k_ntt_inv_big<{ps}>"},
                 "fwd": {"fwd": f"k_ntt_fwd_big<{ps}>"}, "inv": {"inv": f"k_ntt_inv_big<{ps}>"},
-                "polymul": {"mul": f"k_poly_mul_large<{ps}, false>"},
-                "polymul_ntt": {"mulntt": f"k_poly_mul_large<{ps}, true>"}}[op]
+                "polymul": {"mul": f"{mk}<{ps}, false>"},
+                "polymul_ntt": {"mulntt": f"{mk}<{ps}, true>"}}[op]
     return {"fwdinv": {"fwd": f"k_ntt_fwd<{ps}, false>", "inv": f"k_ntt_inv<{ps}, false>"},
             "fwd": {"fwd": f"k_ntt_fwd<{ps}, false>"}, "inv": {"inv": f"k_ntt_inv<{ps}, false>"},
             "polymul": {"mul": f"k_poly_mul<{ps}, false, 0>"}, "polymul_ntt": {"mulntt": f"k_poly_mul<{ps}, true, 0>"},
