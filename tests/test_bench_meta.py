@@ -96,3 +96,21 @@ def test_valu_cost_table_classes():
     assert cost["v_add_u32"] < 3.0 and cost["v_sub_u32"] < 3.0
     for op in ("v_min_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u64_u32", "v_mad_i64_i32"):
         assert 4.0 < cost[op] < 5.0, op
+
+
+@pytest.mark.parametrize("config", [4, 5])
+def test_valu_entry_of_valu_bound_configs(ntt, config):
+    """The committed PMC summary carries the VALU counter entry the config-4 /
+    config-5 lines report as their roofline (tools/valu_summary.py kernel):
+    measured on the same build as the traffic, with a busy fraction a
+    VALU-bound kernel can have."""
+    op, param, batch, ring = bench.CONFIGS[config]
+    info = ntt.param_info(param)
+    workload = bench.workload_name(op, param, info["n"], info["q"], ring)
+    with open(bench.PMC_PATH) as f:
+        e = json.load(f)["entries"][workload]
+    assert op in bench.VALU_BOUND
+    k = next(iter(e["valu"]["kernels"].values()))
+    assert k["SQ_INSTS_VALU"] > 1e9 and 3.0 < k["mean_simd_cycles_per_valu"] < 5.0
+    assert 0.5 < k["valu_busy_at_pmc_clock"] < 1.0
+    assert 1.5 < k["clock_ghz_pmc"] < 2.5
