@@ -40,8 +40,9 @@ extern "C" {
 #define NTT_PARAM_P_III 2 /* n = 2048, q = 856145921, psi = 3^((q-1)/2n)    */
 /* Larger transforms over p-III's prime (q - 1 = 2^14 * 52255 admits
  * negacyclic n up to 8192), for the reference's n > 2048 dataflows (its
- * Stockham / CT2 kernels, NTT.cu:1085-1153, 1268-1337, 667-951): multi-wave
- * four-step kernels.  For these sets every entry point is accepted except
+ * Stockham / CT2 kernels, NTT.cu:1085-1153, 1268-1337, 667-951): one wave
+ * per polynomial (the n = 8192 products: a multi-wave four-step kernel).
+ * For these sets every entry point is accepted except
  * poly_mul_nussbaumer (NTT_ERR_PARAM: its split is defined for n = 1024 /
  * 2048).  poly_mul / poly_mul_ntt are one fused launch; poly_bitrev_copy is
  * one launch; poly_ntt_bitrev / poly_invntt_bitrev are two (the natural-order

@@ -134,12 +134,14 @@ inline hipError_t upload_large_tables(int ps, const Tables &t)
                                    hipMemcpyHostToDevice)) != hipSuccess)
             return e;
     }
-    uint2 last[2][LARGE_GMAX] = {};
+    uint2 last[3][LARGE_GMAX] = {};
     const uint32_t r32 = (uint32_t)((1ull << 32) % p.q);
-    for (int rs = 0; rs < 2; rs++)
-        for (uint32_t B = 0; B < G; B++) {   // n^-1 psi^-brv(G + B) (rs: times 2^32), centred signed
+    for (int rs = 0; rs < 3; rs++)
+        for (uint32_t B = 0; B < G; B++) {   // n^-1 psi^-brv(G + B) (rs 1: times 2^32; rs 2: times 8 2^32,
+                                              // the incomplete-domain product's (n/8)^-1), centred signed
             uint32_t w = (uint32_t)((uint64_t)t.n_inv * t.inv[2 * (G + B)] % p.q);
             if (rs) w = (uint32_t)((uint64_t)w * r32 % p.q);
+            if (rs == 2) w = (uint32_t)((uint64_t)w * 8 % p.q);
             const TwPair c = csigned_tw(w, p.q);
             last[rs][B].x = c.x;
             last[rs][B].y = c.y;

@@ -207,7 +207,7 @@ template <int PS> struct LXform {
 template <int PS, bool BHAT>
 void launch_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s, const DevInfo &d)
 {
-    using LG = Large<PS, mul_large_waves<PS, BHAT>()>;
+    using LG = LargeMul<PS, BHAT>;
     const size_t ppw = large_ppw<LG>(batch, d);
     const dim3 g((uint32_t)((batch + LG::SLOTS * ppw - 1) / (LG::SLOTS * ppw))), blk(LG::NT);
     hipLaunchKernelGGL((k_poly_mul_large<PS, BHAT>), g, blk, 0, s, a, b, c, (uint32_t)batch, (uint32_t)ppw);

@@ -36,7 +36,7 @@ __constant__ uint2 c_subtw[LARGE_NPS][2][LARGE_GMAX][32];
 __constant__ uint2 c_cross[LARGE_NPS][2][4];
 // last sub-tree inverse stage: n^-1 psi^-brv(2^g + B), centred signed pair,
 // [set][plain / times 2^32 (the products' Montgomery factor)][B]
-__constant__ uint2 c_lastinv[LARGE_NPS][2][LARGE_GMAX];
+__constant__ uint2 c_lastinv[LARGE_NPS][3][LARGE_GMAX];
 // LDS images (lane twiddles + bit-5 table) of T_B, [set][fwd/inv][B]; the
 // kernels copy the lane twiddles of B = 0 only (shared, see c_fscale) and the
 // 32-entry bit-5 table of every B
@@ -56,7 +56,7 @@ __device__ uint4 g_tw2imgL[LARGE_NPS][2][LARGE_GMAX][TW2_VEC4];
 // 15.75 KiB LDS images (n = 8192) are freed: 16 waves per workgroup instead of 12.
 __constant__ uint2 c_fscale[LARGE_NPS][2][LARGE_GMAX][32];
 
-template <int PS, int MULW = 0>
+template <int PS, int MULW = 0, bool INC_ = false>
 struct Large {
     using PL = typename PSel<PS>::T;   // the n-point set
     using P = PS2;                     // 2048-point sub-transforms over the same prime
@@ -75,13 +75,20 @@ struct Large {
     // LDS, always the shared lane table.
     static constexpr bool MUL = MULW != 0;
     static constexpr int WAVES = MUL ? MULW : 16;
-    static constexpr bool SHARED = MUL || G == 4;
+    // INC: poly_mul in the incomplete domain (residues mod x^8 -+ zeta, the
+    // n = 2048 product's BaseMul): pass 2 stops at pos bit 3, so a sub-tree's
+    // lane table is only its first three entries (+ its bit-5 table) and every
+    // B keeps its own (no shared table, no sub-tree scaling)
+    static constexpr bool INC = INC_;
+    static constexpr int INC_ENTRIES = 3;
+    static constexpr int CTAB_WORDS = INC_ENTRIES * 64 * 2 + 64;   // compact per-B image
+    static constexpr bool SHARED = !INC && (MUL || G == 4);
     static constexpr int OCC = WAVES / 4;
     static constexpr int SLOTS = WAVES / G;   // polynomials per workgroup step
     static constexpr int NT = WAVES * 64;
     static constexpr int IDX = PS - LARGE_PS0;
     // lane tables (shared: T_0's + per-B bit-5 tables; else G whole images)
-    static constexpr int TAB_WORDS = SHARED ? TW2_WORDS + G * 64 : G * TW2_WORDS;
+    static constexpr int TAB_WORDS = INC ? G * CTAB_WORDS : SHARED ? TW2_WORDS + G * 64 : G * TW2_WORDS;
     static constexpr int NTAB = MUL ? 2 : 1;   // forward table, then (MUL) the inverse's
     static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + NTAB * TAB_WORDS + SLOTS + 1;   // + slot counters, poison word
 };
@@ -303,6 +310,14 @@ template <class LG, bool INV>
 __device__ __forceinline__ void fill_large_tw(uint32_t *tab)
 {
     uint4 *dst = reinterpret_cast<uint4 *>(tab);
+    if constexpr (LG::INC) {   // per B: lane entries 0..2, then the bit-5 table
+        constexpr int LV = LG::INC_ENTRIES * 64 * 2 / 4, CV = LG::CTAB_WORDS / 4;
+        for (int i = threadIdx.x; i < LG::G * CV; i += LG::NT) {
+            const int b = i / CV, o = i % CV;
+            dst[i] = g_tw2imgL[LG::IDX][INV ? 1 : 0][b][o < LV ? o : TW2_BIT5_VEC4 + (o - LV)];
+        }
+        return;
+    }
     if constexpr (!LG::SHARED) {   // the G images, contiguous in g_tw2imgL
         const uint4 *src = g_tw2imgL[LG::IDX][INV ? 1 : 0][0];
         for (int i = threadIdx.x; i < LG::G * TW2_VEC4; i += LG::NT) dst[i] = src[i];
@@ -367,8 +382,13 @@ struct LargeWave {
     template <int D>
     __device__ __forceinline__ void table_ptrs(uint32_t *t)
     {
-        tw2[D] = reinterpret_cast<const uint2 *>(t + (LG::SHARED ? 0u : B * TW2_WORDS));
-        bit5[D] = LG::SHARED ? reinterpret_cast<const uint2 *>(t + TW2_BIT5_VEC4 * 4 + B * 64) : tw2[D] + TW2_ENTRIES * 64;
+        if constexpr (LG::INC) {
+            tw2[D] = reinterpret_cast<const uint2 *>(t + B * LG::CTAB_WORDS);
+            bit5[D] = tw2[D] + LG::INC_ENTRIES * 64;
+        } else {
+            tw2[D] = reinterpret_cast<const uint2 *>(t + (LG::SHARED ? 0u : B * TW2_WORDS));
+            bit5[D] = LG::SHARED ? reinterpret_cast<const uint2 *>(t + TW2_BIT5_VEC4 * 4 + B * 64) : tw2[D] + TW2_ENTRIES * 64;
+        }
     }
     // Re-derive the wave-uniform state from an opaque wave index at the top of
     // every step: otherwise every address, table pointer and branch mask
@@ -398,6 +418,7 @@ struct LargeWave {
     // of global index G k' + brv_g(B), in [0,4q)
     // (LARGE_HEAD: the input is in the head's chunked layout instead, see
     // head_fwd, and the first g stages run in registers + one exchange)
+    template <int BMIN = 0>
     __device__ __forceinline__ void fwd(uint32_t (&r)[32])
     {
         constexpr int G = LG::G;
@@ -413,7 +434,7 @@ struct LargeWave {
         fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), bit5[0] + opaque_zero());
         lds_p1_to_p2<P>(r, buf, LT(opaque_lane()));   // addresses recomputed (see inv)
         subtree_scale<P, LG, false>(r, B);             // T_B = c_{B,b} T_0 (c_fscale)
-        fwd_pass2<P>(r, tw2[0] + opaque_zero(), L.lane);
+        fwd_pass2<P, BMIN>(r, tw2[0] + opaque_zero(), L.lane);
     }
     // all-to-all through the exchange buffers: from the pass-2 layout to
     // global words [2048 B, 2048 B + 2048) at register j of lane l = word
@@ -454,19 +475,22 @@ struct LargeWave {
     // inverse from the pass-2 layout (inputs < 2q) to this wave's share of
     // the natural order (word 2048 B + 64 j + brl at register j), [0,2q),
     // scaled by n^-1 (RS: and by 2^32, undoing a Montgomery product's 2^-32)
-    template <bool RS>
+    // RS 0: plain inverse; 1: also times 2^32 (undoes a Montgomery product's
+    // 2^-32); 2: the incomplete-domain product's -- from pos bit BMIN (WIDE0:
+    // BaseMul's wide outputs), scaled by (n/2^BMIN)^-1 2^32
+    template <int RS, int BMIN = 0, bool WIDE0 = false>
     __device__ __forceinline__ void inv(uint32_t (&r)[32])
     {
         constexpr int G = LG::G;
-        constexpr uint32_t NINV = RS ? LG::PL::NINV_R : LG::PL::NINV;
+        constexpr uint32_t NINV = RS == 2 ? LG::PL::template ninv_r<BMIN>() : RS ? LG::PL::NINV_R : LG::PL::NINV;
         constexpr uint32_t NINVP = cshoup(NINV, P::Q);
-        inv_pass2<P>(r, tw2[1] + opaque_zero(), L.lane);
+        inv_pass2<P, BMIN, WIDE0>(r, tw2[1] + opaque_zero(), L.lane);
         subtree_scale<P, LG, true>(r, B);   // the c'_{B,b} the shared table left out (c_fscale)
         // transpose addresses from an opaque lane: recomputed here instead of
         // 8 loop-invariant VGPRs (which spilled at the 128-VGPR budget)
         lds_p2_to_p1<P>(r, buf, LT(opaque_lane()));
         inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5[1] + opaque_zero());
-        const uint2 last = c_lastinv[LG::IDX][RS ? 1 : 0][B];
+        const uint2 last = c_lastinv[LG::IDX][RS][B];
         inv_last_stage<P, false>(r, NINV, NINVP, last.x, last.y);   // [0,2q)
         if constexpr (LARGE_HEAD) {   // output in the head's chunked layout
             head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, opaque_lane(), B, ss);
@@ -541,16 +565,27 @@ __device__ __forceinline__ void large_store(uint32_t *dst, const LargeWave<LG> &
                               // in-register head 12 waves spill 5: 6.09 -> 5.93 ms per 2^17 products
                               // (profiles/r03/ab_mul_large_w12.log)
 #endif
+#ifndef MUL_LARGE_INC
+#define MUL_LARGE_INC 1   // poly_mul (not poly_mul_ntt) in the incomplete domain
+#endif
+template <int PS, bool BHAT>
+constexpr bool mul_large_inc()
+{
+    return !BHAT && MUL_LARGE_INC;
+}
 template <int PS, bool BHAT>
 constexpr int mul_large_waves()
 {
-    return (PSel<PS>::T::N == 8192 && !BHAT) ? MUL_LARGE_WAVES : 12;
+    // the incomplete domain's compact tables leave room for 16 waves (4 per SIMD)
+    return mul_large_inc<PS, BHAT>() ? 16 : (PSel<PS>::T::N == 8192 && !BHAT) ? MUL_LARGE_WAVES : 12;
 }
 template <int PS, bool BHAT>
-__global__ __launch_bounds__((Large<PS, mul_large_waves<PS, BHAT>()>::NT), (Large<PS, mul_large_waves<PS, BHAT>()>::OCC))
+using LargeMul = Large<PS, mul_large_waves<PS, BHAT>(), mul_large_inc<PS, BHAT>()>;
+template <int PS, bool BHAT>
+__global__ __launch_bounds__((LargeMul<PS, BHAT>::NT), (LargeMul<PS, BHAT>::OCC))
 void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
 {
-    using LG = Large<PS, mul_large_waves<PS, BHAT>()>;
+    using LG = LargeMul<PS, BHAT>;
     using P = typename LG::P;
     constexpr bool PF = MUL_PF && !(LG::G == 4 && !BHAT);
     __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
@@ -570,7 +605,9 @@ void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_
         // through b's transform)
         load32(ra, a + base + opaque_lane(), [](int j) { return large_off<LG>(j); });
         if (PF) load32(rb, b + bbase + opaque_lane(), boff);
-        w.fwd(ra);
+        constexpr int LOGR = LG::INC ? mul_logr<2>() : 0;
+        using BM = BaseMul<P, mul_logr<2>()>;
+        w.template fwd<LOGR>(ra);
 #pragma unroll
         for (int j = 0; j < 32; ++j) asm volatile("" : "+v"(ra[j]));   // phase boundary (register pressure)
         if (!PF) load32(rb, b + bbase + opaque_lane(), boff);
@@ -580,10 +617,15 @@ void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_
             w.ss.template wait<LG::G>();
             w.from_contiguous(rb);
         }
-        else w.fwd(rb);
+        else w.template fwd<LOGR>(rb);
+        if constexpr (LG::INC) {
+            BM::run(ra, rb, w.tw2[0] + opaque_zero(), w.L.lane);
+            w.template inv<2, LOGR, BM::WIDE>(ra);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(csub<P::Q2>(ra[j]), csub<P::Q2>(rb[j]));
-        w.template inv<true>(ra);
+            for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(csub<P::Q2>(ra[j]), csub<P::Q2>(rb[j]));
+            w.template inv<1>(ra);
+        }
         if (valid) large_store(c + base + opaque_lane(), w, [&](int j) { return csub<P::Q>(ra[j]); });
     };
     large_steps(w, first, npoly, ppw, step);
