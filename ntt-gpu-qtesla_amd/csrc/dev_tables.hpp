@@ -84,12 +84,16 @@ inline hipError_t upload_large_tables(int ps, const Tables &t)
     const uint32_t G = p.n / 2048;
     hipError_t e;
     for (int inv = 0; inv < 2; inv++) {
-        uint2 sub[LARGE_GMAX][32] = {}, cross[4] = {};
+        uint2 sub[LARGE_GMAX][32] = {}, cross[4] = {}, b5[LARGE_GMAX][32] = {};
         for (uint32_t B = 0; B < G; B++) {
             for (uint32_t kp = 0; kp < 32; kp++)
                 dev_pair(p, t, inv != 0, sub_tree_k(kp, G, B), sub[B][kp].x, sub[B][kp].y);
             const std::vector<uint32_t> img =
                 dev_tw2_image(p, t, inv != 0, 11, [&](uint32_t kp) { return sub_tree_k(kp, G, B); });
+            for (int i = 0; i < 32; i++) {   // the image's bit-5 pairs (c_bit5L)
+                b5[B][i].x = img[TW2_BIT5_VEC4 * 4 + 2 * i];
+                b5[B][i].y = img[TW2_BIT5_VEC4 * 4 + 2 * i + 1];
+            }
             const size_t off = ((size_t)(idx * 2 + inv) * LARGE_GMAX + B) * TW2_VEC4 * 16;
             if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_tw2imgL), img.data(), TW2_WORDS * 4, off, hipMemcpyHostToDevice)) !=
                 hipSuccess)
@@ -131,6 +135,9 @@ inline hipError_t upload_large_tables(int ps, const Tables &t)
                                    hipMemcpyHostToDevice)) != hipSuccess)
             return e;
         if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_cross), cross, sizeof cross, (size_t)(idx * 2 + inv) * sizeof cross,
+                                   hipMemcpyHostToDevice)) != hipSuccess)
+            return e;
+        if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_bit5L), b5, sizeof b5, (size_t)(idx * 2 + inv) * sizeof b5,
                                    hipMemcpyHostToDevice)) != hipSuccess)
             return e;
     }

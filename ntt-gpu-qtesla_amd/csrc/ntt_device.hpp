@@ -351,7 +351,20 @@ __device__ __forceinline__ void fill_tw2(uint2 *tab)
 // `tw` = the uniform twiddles k < 32 (wave-uniform pointer), `sw` = the
 // 32-entry bit-5 table in LDS.  RED0: inputs in [0,4q) (stage 0 reduces too);
 // otherwise inputs < 2q.
-template <class P, bool RED0 = false>
+// USW: `sw` is a wave-uniform (__constant__) bit-5 table; the lane-half
+// twiddle is selected per lane from the two scalar-loaded candidates
+template <bool USW>
+__device__ __forceinline__ uint2 bit5_tw(const uint2 *sw, int m, uint32_t h)
+{
+    if constexpr (USW) {
+        const uint2 w0 = sw[2 * m], w1 = sw[2 * m + 1];
+        return make_uint2(h ? w1.x : w0.x, h ? w1.y : w0.y);
+    } else {
+        return sw[2 * m + h];
+    }
+}
+
+template <class P, bool RED0 = false, bool USW = false>
 __device__ __forceinline__ void fwd_pass1_tw(uint32_t (&r)[32], uint32_t h, const uint2 *tw, const uint2 *sw)
 {
 #pragma unroll
@@ -374,7 +387,7 @@ __device__ __forceinline__ void fwd_pass1_tw(uint32_t (&r)[32], uint32_t h, cons
             const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
             r[2 * m] = pr[0];
             r[2 * m + 1] = pr[1];
-            const uint2 w = sw[2 * m + h];   // k = 32 + 2m + h
+            const uint2 w = bit5_tw<USW>(sw, m, h);   // k = 32 + 2m + h
             ct_bfly<P::Q>(r[2 * m], r[2 * m + 1], w.x, w.y);
         }
     }
@@ -717,13 +730,13 @@ struct NoEmit {
 // inverse pass 1 without its last stage: (n=2048) GS on pos bit 5 + swap
 // back, then the GS stages on pos bits LOGN-5 .. LOGN-2 (j bits 0..3); `tw` =
 // the uniform twiddles k < 32.
-template <class P>
+template <class P, bool USW = false>
 __device__ __forceinline__ void inv_pass1_head(uint32_t (&r)[32], uint32_t h, const uint2 *tw, const uint2 *sw)
 {
     if constexpr (P::LOGN == 11) {
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
-            const uint2 w = sw[2 * m + h];
+            const uint2 w = bit5_tw<USW>(sw, m, h);
             gs_bfly<P::Q>(r[2 * m], r[2 * m + 1], w.x, w.y);
             const auto pr = __builtin_amdgcn_permlane32_swap(r[2 * m], r[2 * m + 1], false, false);
             r[2 * m] = pr[0];

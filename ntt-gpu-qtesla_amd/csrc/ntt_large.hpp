@@ -37,6 +37,9 @@ __constant__ uint2 c_cross[LARGE_NPS][2][4];
 // last sub-tree inverse stage: n^-1 psi^-brv(2^g + B), centred signed pair,
 // [set][plain / times 2^32 (the products' Montgomery factor)][B]
 __constant__ uint2 c_lastinv[LARGE_NPS][3][LARGE_GMAX];
+// bit-5 pairs of every sub-tree [set][fwd/inv][B][32] for kernels that keep
+// them out of LDS (Large::BIT5U)
+__constant__ uint2 c_bit5L[LARGE_NPS][2][LARGE_GMAX][32];
 // LDS images (lane twiddles + bit-5 table) of T_B, [set][fwd/inv][B]; the
 // kernels copy the lane twiddles of B = 0 only (shared, see c_fscale) and the
 // 32-entry bit-5 table of every B
@@ -56,7 +59,9 @@ __device__ uint4 g_tw2imgL[LARGE_NPS][2][LARGE_GMAX][TW2_VEC4];
 // 15.75 KiB LDS images (n = 8192) are freed: 16 waves per workgroup instead of 12.
 __constant__ uint2 c_fscale[LARGE_NPS][2][LARGE_GMAX][32];
 
-template <int PS, int MULW = 0, bool INC_ = false>
+constexpr int TW2_BIT5_VEC4 = TW2_ENTRIES * 64 * 2 / 4;   // uint4 offset of the bit-5 table in an image
+
+template <int PS, int MULW = 0, bool INC_ = false, bool BIT5U_ = false>
 struct Large {
     using PL = typename PSel<PS>::T;   // the n-point set
     using P = PS2;                     // 2048-point sub-transforms over the same prime
@@ -88,7 +93,12 @@ struct Large {
     static constexpr int NT = WAVES * 64;
     static constexpr int IDX = PS - LARGE_PS0;
     // lane tables (shared: T_0's + per-B bit-5 tables; else G whole images)
-    static constexpr int TAB_WORDS = INC ? G * CTAB_WORDS : SHARED ? TW2_WORDS + G * 64 : G * TW2_WORDS;
+    // BIT5U: the sub-trees' bit-5 pairs from __constant__ memory (c_bit5L,
+    // per-lane select of two scalar-loaded candidates) instead of LDS: the
+    // shared table alone then leaves room for 16 waves
+    static constexpr bool BIT5U = BIT5U_;
+    static_assert(!BIT5U || (SHARED && !INC), "BIT5U: shared-table kernels only");
+    static constexpr int TAB_WORDS = INC ? G * CTAB_WORDS : SHARED ? (BIT5U ? TW2_BIT5_VEC4 * 4 : TW2_WORDS + G * 64) : G * TW2_WORDS;
     static constexpr int NTAB = MUL ? 2 : 1;   // forward table, then (MUL) the inverse's
     static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + NTAB * TAB_WORDS + SLOTS + 1;   // + slot counters, poison word
 };
@@ -305,7 +315,6 @@ __device__ __forceinline__ uint32_t xch_pos(uint32_t kp, uint32_t B)
 
 // The workgroup's twiddle tables of one direction into LDS at `tab`: T_0's
 // lane image, then the bit-5 table of every B (SHARED), else the G images.
-constexpr int TW2_BIT5_VEC4 = TW2_ENTRIES * 64 * 2 / 4;   // uint4 offset of the bit-5 table in an image
 template <class LG, bool INV>
 __device__ __forceinline__ void fill_large_tw(uint32_t *tab)
 {
@@ -323,7 +332,7 @@ __device__ __forceinline__ void fill_large_tw(uint32_t *tab)
         for (int i = threadIdx.x; i < LG::G * TW2_VEC4; i += LG::NT) dst[i] = src[i];
         return;
     }
-    for (int i = threadIdx.x; i < TW2_BIT5_VEC4 + LG::G * 16; i += LG::NT) {
+    for (int i = threadIdx.x; i < TW2_BIT5_VEC4 + (LG::BIT5U ? 0 : LG::G * 16); i += LG::NT) {
         const int b = i < TW2_BIT5_VEC4 ? 0 : (i - TW2_BIT5_VEC4) >> 4;
         const int o = i < TW2_BIT5_VEC4 ? i : TW2_BIT5_VEC4 + ((i - TW2_BIT5_VEC4) & 15);
         dst[i] = g_tw2imgL[LG::IDX][INV ? 1 : 0][b][o];
@@ -385,6 +394,9 @@ struct LargeWave {
         if constexpr (LG::INC) {
             tw2[D] = reinterpret_cast<const uint2 *>(t + B * LG::CTAB_WORDS);
             bit5[D] = tw2[D] + LG::INC_ENTRIES * 64;
+        } else if constexpr (LG::BIT5U) {
+            tw2[D] = reinterpret_cast<const uint2 *>(t);
+            bit5[D] = c_bit5L[LG::IDX][D][B];
         } else {
             tw2[D] = reinterpret_cast<const uint2 *>(t + (LG::SHARED ? 0u : B * TW2_WORDS));
             bit5[D] = LG::SHARED ? reinterpret_cast<const uint2 *>(t + TW2_BIT5_VEC4 * 4 + B * 64) : tw2[D] + TW2_ENTRIES * 64;
@@ -431,7 +443,7 @@ struct LargeWave {
             if constexpr (G == 4)
                 cross_ct<P, true, G>(r, buf, partner(1u), opaque_lane(), (B & 1u) != 0, c_cross[LG::IDX][0][2 + (B >> 1)], ss);
         }
-        fwd_pass1_tw<P, true>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), bit5[0] + opaque_zero());
+        fwd_pass1_tw<P, true, LG::BIT5U>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), bit5[0] + opaque_zero());
         lds_p1_to_p2<P>(r, buf, LT(opaque_lane()));   // addresses recomputed (see inv)
         subtree_scale<P, LG, false>(r, B);             // T_B = c_{B,b} T_0 (c_fscale)
         fwd_pass2<P, BMIN>(r, tw2[0] + opaque_zero(), L.lane);
@@ -489,7 +501,7 @@ struct LargeWave {
         // transpose addresses from an opaque lane: recomputed here instead of
         // 8 loop-invariant VGPRs (which spilled at the 128-VGPR budget)
         lds_p2_to_p1<P>(r, buf, LT(opaque_lane()));
-        inv_pass1_head<P>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5[1] + opaque_zero());
+        inv_pass1_head<P, LG::BIT5U>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5[1] + opaque_zero());
         const uint2 last = c_lastinv[LG::IDX][RS][B];
         inv_last_stage<P, false>(r, NINV, NINVP, last.x, last.y);   // [0,2q)
         if constexpr (LARGE_HEAD) {   // output in the head's chunked layout
@@ -573,14 +585,25 @@ constexpr bool mul_large_inc()
 {
     return !BHAT && MUL_LARGE_INC;
 }
+#ifndef MUL_LARGE_BIT5U
+#define MUL_LARGE_BIT5U 1   // poly_mul_ntt: bit-5 pairs from __constant__, 16 waves
+#endif
+template <int PS, bool BHAT>
+constexpr bool mul_large_bit5u()
+{
+    return BHAT && MUL_LARGE_BIT5U;
+}
 template <int PS, bool BHAT>
 constexpr int mul_large_waves()
 {
-    // the incomplete domain's compact tables leave room for 16 waves (4 per SIMD)
-    return mul_large_inc<PS, BHAT>() ? 16 : (PSel<PS>::T::N == 8192 && !BHAT) ? MUL_LARGE_WAVES : 12;
+    // the incomplete domain's compact tables, or the shared table without its
+    // bit-5 pairs, leave room for 16 waves (4 per SIMD)
+    return (mul_large_inc<PS, BHAT>() || mul_large_bit5u<PS, BHAT>()) ? 16
+           : (PSel<PS>::T::N == 8192 && !BHAT)                         ? MUL_LARGE_WAVES
+                                                                       : 12;
 }
 template <int PS, bool BHAT>
-using LargeMul = Large<PS, mul_large_waves<PS, BHAT>(), mul_large_inc<PS, BHAT>()>;
+using LargeMul = Large<PS, mul_large_waves<PS, BHAT>(), mul_large_inc<PS, BHAT>(), mul_large_bit5u<PS, BHAT>()>;
 template <int PS, bool BHAT>
 __global__ __launch_bounds__((LargeMul<PS, BHAT>::NT), (LargeMul<PS, BHAT>::OCC))
 void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
