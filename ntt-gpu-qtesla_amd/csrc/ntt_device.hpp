@@ -870,8 +870,21 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
 #ifndef MUL_WAVES_PER_SIMD
 #define MUL_WAVES_PER_SIMD 4
 #endif
-template <int PS> constexpr int mul_wg() { return MUL_WG; }
+// MUL_COMPACT: poly_mul (not poly_mul_ntt) reads only lane-table entries
+// 0..2 (pass 2 stops at pos bit 3; BaseMul's zeta are entries 1, 2) and the
+// bit-5 pairs, so its workgroup keeps just those (compact tables: 3.5 KiB for
+// both directions instead of 31.5) and runs as two 8-wave workgroups per CU
+// (same 4 waves/SIMD): the CU no longer drains to start the next workgroup.
+// p-III 7.69 -> 7.35 ms, p-I 3.46 -> 3.25 ms per 2^20 (profiles/r04/r/)
+#ifndef MUL_COMPACT
+#define MUL_COMPACT 1
+#endif
+template <int PS, bool BHAT> constexpr bool mul_compact() { return MUL_COMPACT && !BHAT; }
+template <int PS, bool BHAT = false> constexpr int mul_wg() { return mul_compact<PS, BHAT>() ? 512 : MUL_WG; }
 template <int PS> constexpr int mul_occ() { return MUL_WAVES_PER_SIMD; }
+constexpr int MUL_CENT = 3;   // lane-table entries a compact table keeps
+// compact table image: entries 0..MUL_CENT-1 (L lanes each), then the 32 bit-5 pairs
+template <class P> constexpr int mul_ctab_words() { return MUL_CENT * (int)tw2_lanes<P>() * 2 + 64; }
 template <int PS> constexpr int mul_logr() { return PSel<PS>::T::LOGN == 11 ? MUL_LOGR : MUL_LOGR_SMALL; }
 constexpr int WG = 256;   // elementwise kernels
 constexpr int NTT_WAVES = NTT_WG / 64;
@@ -1022,18 +1035,37 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_bitrev(const uin
 // VAR (tools/ntt_diag.hip only, bottleneck attribution): 1 = global loads
 // and stores only (no arithmetic, no LDS), 2 = arithmetic + LDS only
 // (register-made inputs, outputs kept live, nothing stored).
+// compact copy of a direction's image (MUL_COMPACT)
+template <int PS, bool INV, int NT>
+__device__ __forceinline__ void fill_tw2_compact(uint2 *tab)
+{
+    using P = typename PSel<PS>::T;
+    constexpr int LV = MUL_CENT * (int)tw2_lanes<P>() * 2 / 4, CV = mul_ctab_words<P>() / 4;
+    const uint4 *src = g_tw2img[PS][INV ? 1 : 0];
+    uint4 *dst = reinterpret_cast<uint4 *>(tab);
+    for (int i = threadIdx.x; i < CV; i += NT) dst[i] = src[i < LV ? i : TW2_ENTRIES * 64 * 2 / 4 + (i - LV)];
+}
+
 template <int PS, bool BHAT, int VAR = 0>
-__global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
+__global__ __launch_bounds__((mul_wg<PS, BHAT>()), mul_occ<PS>()) void k_poly_mul(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
 {
     using P = typename PSel<PS>::T;
     using LT = Lane<P>;
-    constexpr int WG_ = mul_wg<PS>();
+    constexpr bool CMP = mul_compact<PS, BHAT>();
+    constexpr int WG_ = mul_wg<PS, BHAT>();
     constexpr int WAVES = WG_ / 64;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + 2 * TW2_WORDS];
+    constexpr int TABW = CMP ? mul_ctab_words<P>() : TW2_WORDS;   // words per direction
+    constexpr int SWO = CMP ? MUL_CENT * (int)tw2_lanes<P>() : TW2_ENTRIES * 64;   // bit-5 pairs' offset (pairs)
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WAVES * XPOSE_WORDS + 2 * TABW];
     uint2 *ftw2 = reinterpret_cast<uint2 *>(lds + WAVES * XPOSE_WORDS);
-    uint2 *itw2 = ftw2 + TW2_WORDS / 2;
-    fill_tw2<PS, false, WG_>(ftw2);
-    fill_tw2<PS, true, WG_>(itw2);
+    uint2 *itw2 = ftw2 + TABW / 2;
+    if constexpr (CMP) {
+        fill_tw2_compact<PS, false, WG_>(ftw2);
+        fill_tw2_compact<PS, true, WG_>(itw2);
+    } else {
+        fill_tw2<PS, false, WG_>(ftw2);
+        fill_tw2<PS, true, WG_>(itw2);
+    }
     __syncthreads();
     const LT L;
     uint32_t *buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
@@ -1069,8 +1101,8 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
             continue;
         }
         constexpr bool LZ = !BHAT && MUL_LAZYBIAS;   // typed forwards (fwd_pass1_lz)
-        if constexpr (LZ) fwd_pass1_lz<P>(ra, L.h, tw_base<PS, false>(), ftw2 + TW2_ENTRIES * 64 + opaque_zero());
-        else fwd_pass1<PS, P>(ra, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+        if constexpr (LZ) fwd_pass1_lz<P>(ra, L.h, tw_base<PS, false>(), ftw2 + SWO + opaque_zero());
+        else fwd_pass1<PS, P>(ra, L.h, ftw2 + SWO + opaque_zero());
         // b-hat product: n = 2048 keeps the hoisted addresses, n = 1024 (32-lane
         // twiddle table) recomputes them (hoisted: 22 spilled VGPRs)
         constexpr bool HOIST = BHAT ? P::LOGN == 11 : MUL_HOIST;
@@ -1094,21 +1126,21 @@ __global__ __launch_bounds__(mul_wg<PS>(), mul_occ<PS>()) void k_poly_mul(const 
             // incomplete domain: both forwards stop above pos bit LOGR-1,
             // products mod x^(2^LOGR) -+ zeta, the inverse starts at pos bit
             // LOGR (BaseMul)
-            if constexpr (LZ) fwd_pass1_lz<P>(rb, L.h, tw_base<PS, false>(), ftw2 + TW2_ENTRIES * 64 + opaque_zero());
-            else fwd_pass1<PS, P>(rb, L.h, ftw2 + TW2_ENTRIES * 64 + opaque_zero());
+            if constexpr (LZ) fwd_pass1_lz<P>(rb, L.h, tw_base<PS, false>(), ftw2 + SWO + opaque_zero());
+            else fwd_pass1<PS, P>(rb, L.h, ftw2 + SWO + opaque_zero());
             lds_p1_to_p2<P>(rb, buf, MUL_HOIST ? L : LT(opaque_lane()));
             if constexpr (LZ) fwd_pass2_lz<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
             else fwd_pass2<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
             BaseMul<P, mul_logr<PS>()>::template run<LZ>(ra, rb, ftw2 + opaque_zero(), L.lane);
             inv_pass2<P, mul_logr<PS>(), BaseMul<P, mul_logr<PS>()>::WIDE>(ra, itw2 + opaque_zero(), L.lane);
             lds_p2_to_p1<P>(ra, buf, MUL_HOIST ? L : LT(opaque_lane()));
-            inv_pass1<PS, P, P::template ninv_r<mul_logr<PS>()>(), P::template c1_r<mul_logr<PS>()>()>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
+            inv_pass1<PS, P, P::template ninv_r<mul_logr<PS>()>(), P::template c1_r<mul_logr<PS>()>()>(ra, L.h, itw2 + SWO + opaque_zero(), emit);
         } else {
 #pragma unroll
             for (int j = 0; j < 32; ++j) ra[j] = mont_mul<P>(csub<P::Q2>(ra[j]), csub<P::Q2>(rb[j]));   // b-hat < 2q
             inv_pass2<P>(ra, itw2 + opaque_zero(), L.lane);
             lds_p2_to_p1<P>(ra, buf, HOIST ? L : LT(opaque_lane()));
-            inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + TW2_ENTRIES * 64 + opaque_zero(), emit);
+            inv_pass1<PS, P, P::NINV_R, P::C1_R>(ra, L.h, itw2 + SWO + opaque_zero(), emit);
         }
     }
 }

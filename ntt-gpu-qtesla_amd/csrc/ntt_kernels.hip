@@ -98,11 +98,11 @@ struct Launch {
     uint32_t grid, ppw;
 };
 enum Op { OP_XFORM, OP_MUL };
-Launch launch_for(Op op, int ps, size_t npoly, const DevInfo &d)
+Launch launch_for(Op op, int ps, size_t npoly, const DevInfo &d, int wg = 0)
 {
     const size_t upw = param_set(ps)->logn == 11 ? 1 : 2;
     const size_t units = (npoly + upw - 1) / upw;
-    const size_t waves = (size_t)(op == OP_MUL ? MUL_WG : NTT_WG) / 64;
+    const size_t waves = (size_t)(wg ? wg : op == OP_MUL ? MUL_WG : NTT_WG) / 64;
     const size_t min_groups = (size_t)d.cus * NTT_MIN_WG_PER_CU;
     size_t ppw = units / (waves * min_groups);
     ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
@@ -230,10 +230,13 @@ template <int PS> struct LMul {
             else launch_mul_large<PS, false>(a, b, c, batch, s, d);
             return finish_launch();
         } else {
-            const Launch l = launch_for(OP_MUL, PS, batch, d);
-            const dim3 g(l.grid), blk(mul_wg<PS>());
-            if (bhat) hipLaunchKernelGGL((k_poly_mul<PS, true>), g, blk, 0, s, a, b, c, (uint32_t)batch, l.ppw);
-            else hipLaunchKernelGGL((k_poly_mul<PS, false>), g, blk, 0, s, a, b, c, (uint32_t)batch, l.ppw);
+            if (bhat) {
+                const Launch l = launch_for(OP_MUL, PS, batch, d, mul_wg<PS, true>());
+                hipLaunchKernelGGL((k_poly_mul<PS, true>), dim3(l.grid), dim3(mul_wg<PS, true>()), 0, s, a, b, c, (uint32_t)batch, l.ppw);
+            } else {
+                const Launch l = launch_for(OP_MUL, PS, batch, d, mul_wg<PS, false>());
+                hipLaunchKernelGGL((k_poly_mul<PS, false>), dim3(l.grid), dim3(mul_wg<PS, false>()), 0, s, a, b, c, (uint32_t)batch, l.ppw);
+            }
             return finish_launch();
         }
     }
@@ -450,7 +453,7 @@ int ntt_build_info(char *buf, size_t len)
         "qtesla_ntt gfx950: 1 launch/op, wave-per-poly (n=2048) / half-wave-per-poly (n=1024), 32 coeff/lane, "
         "LDS XOR-swizzled transpose, permlane32 bit-5 stage, Shoup/Harvey lazy CT + signed-Shoup GS butterflies, "
         "dispatch-ordered unit chunks; wg=" QNTT_STR(NTT_WG)
-        " mul_wg=" QNTT_STR(MUL_WG) " ppw<=" QNTT_STR(NTT_PPW_MAX)
+        " mul_wg=" QNTT_STR(MUL_WG) " mul_compact=" QNTT_STR(MUL_COMPACT) " ppw<=" QNTT_STR(NTT_PPW_MAX)
         " min_wg/cu=" QNTT_STR(NTT_MIN_WG_PER_CU) "; src=" QNTT_SRC_HASH;
     const int n = (int)strlen(s);
     if (!buf || !len) return n;
