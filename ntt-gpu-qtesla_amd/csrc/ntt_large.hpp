@@ -585,6 +585,9 @@ constexpr bool mul_large_inc()
 {
     return !BHAT && MUL_LARGE_INC;
 }
+#ifndef MUL_LARGE_INC_WAVES
+#define MUL_LARGE_INC_WAVES 8   // two 8-wave workgroups per CU (78 KiB LDS each): no full-CU drain between workgroups
+#endif
 #ifndef MUL_LARGE_BIT5U
 #define MUL_LARGE_BIT5U 1   // poly_mul_ntt: bit-5 pairs from __constant__, 16 waves
 #endif
@@ -596,9 +599,10 @@ constexpr bool mul_large_bit5u()
 template <int PS, bool BHAT>
 constexpr int mul_large_waves()
 {
-    // the incomplete domain's compact tables, or the shared table without its
-    // bit-5 pairs, leave room for 16 waves (4 per SIMD)
-    return (mul_large_inc<PS, BHAT>() || mul_large_bit5u<PS, BHAT>()) ? 16
+    // the incomplete domain's compact tables leave room for two 8-wave
+    // workgroups per CU (4 waves per SIMD, 4.92 -> 4.55 ms per 2^20 products,
+    // profiles/r04/s); the shared table without its bit-5 pairs for 16 waves
+    return mul_large_inc<PS, BHAT>() ? MUL_LARGE_INC_WAVES : mul_large_bit5u<PS, BHAT>() ? 16
            : (PSel<PS>::T::N == 8192 && !BHAT)                         ? MUL_LARGE_WAVES
                                                                        : 12;
 }
