@@ -108,9 +108,11 @@ def test_large_nussbaumer_unsupported(ntt, dev):
 @pytest.mark.parametrize("ps", LARGE_SETS)
 @pytest.mark.parametrize("batch", [1, 2, 5, 7, 64, 389])
 def test_large_poly_mul_random(ntt, oracle, dev, ps, batch):
-    """Fused product (k_poly_mul_large): partial and full workgroup steps
-    (SLOTS = 6 / 3 polynomials per step on the 12-wave workgroups), bit-exact
-    against the oracle."""
+    """Fused products, bit-exact against the oracle, over partial and full
+    workgroup steps: n = 4096 on k_poly_mul_big (one wave per product, 8 per
+    workgroup), n = 8192 on k_poly_mul_large (poly_mul: 4 products per step on
+    8-wave workgroups; poly_mul_ntt: 8 on 16-wave ones) -- 5, 7 and 389 are
+    multiples of none of them."""
     a = oracle.fill_uniform(batch, ps, 0x3A + batch, 0)
     b = oracle.fill_uniform(batch, ps, 0x3B + batch, 0)
     ta, tb = _dev(ntt, a, dev), _dev(ntt, b, dev)
