@@ -70,7 +70,7 @@ __constant__ uint2 c_bigtw[LARGE_NPS][2][BIG_RMAX];
 // the R bit-5 pairs, [set][fwd/inv]
 __device__ uint4 g_bigimg[LARGE_NPS][2][BIG_IMG_VEC4_MAX];
 
-template <int PS, int WV = 0>
+template <int PS, int WV = 0, bool CMP = false>
 struct Big {
     using PL = typename PSel<PS>::T;   // the n-point set
     using P = PS2;                     // same prime; butterflies only use Q
@@ -89,6 +89,12 @@ struct Big {
     static constexpr int IMG_WORDS = 2 * (LANE_PAIRS + R);         // + bit-5 table
     static constexpr int IMG_VEC4 = IMG_WORDS / 4;
     static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + IMG_WORDS;
+    // CMP (the products' incomplete domain): per chunk only lane entries
+    // 0 .. MUL_CENT-1, then the bit-5 pairs -- TS pairs per chunk, the bit-5
+    // pairs at SWO, TAB_WORDS per direction
+    static constexpr int TS = CMP ? MUL_CENT * 64 : TW2_ENTRIES * 64;
+    static constexpr int SWO = CMP ? CH * TS : LANE_PAIRS;
+    static constexpr int TAB_WORDS = CMP ? 2 * (CH * TS + R) : IMG_WORDS;
     static_assert(IMG_VEC4 <= BIG_IMG_VEC4_MAX, "image size");
     static_assert(LDS_WORDS * 4 <= 160 * 1024, "one workgroup per CU");
     // register of transposition row t of chunk c (layout A'')
@@ -149,6 +155,12 @@ __device__ __forceinline__ void fill_big_tw(uint32_t *tab)
 {
     const uint4 *src = g_bigimg[BG::IDX][INV ? 1 : 0];
     uint4 *dst = reinterpret_cast<uint4 *>(tab);
+    if constexpr (BG::TS != TW2_ENTRIES * 64) {   // gather the compact image
+        constexpr int CV = BG::TS * 2 / 4, SV = TW2_ENTRIES * 64 * 2 / 4;
+        for (int i = threadIdx.x; i < BG::TAB_WORDS / 4; i += BG::NT)
+            dst[i] = src[i < BG::CH * CV ? (i / CV) * SV + i % CV : BG::LANE_PAIRS * 2 / 4 + (i - BG::CH * CV)];
+        return;
+    }
     for (int i = threadIdx.x; i < BG::IMG_VEC4; i += BG::NT) dst[i] = src[i];
 }
 
@@ -204,7 +216,7 @@ __device__ __forceinline__ void big_fwd(uint32_t (&r)[BG::R], uint32_t *buf, con
 {
     using P = typename BG::P;
     big_fwd_pass1<BG>(r);
-    big_fwd_bit5<BG>(r, tab + BG::LANE_PAIRS + opaque_zero(), h);
+    big_fwd_bit5<BG>(r, tab + BG::SWO + opaque_zero(), h);
     sfor<BG::CH>([&](auto C) {
         constexpr int c = C;
         // transpose addresses recomputed per chunk from an opaque lane
@@ -222,7 +234,7 @@ __device__ __forceinline__ void big_fwd(uint32_t (&r)[BG::R], uint32_t *buf, con
             v[4 * Q + 3] = x.w;
         });
         compiler_fence();
-        fwd_pass2<P, BMIN>(v, tab + TW2_ENTRIES * 64 * c + opaque_zero(), lane);
+        fwd_pass2<P, BMIN>(v, tab + BG::TS * c + opaque_zero(), lane);
         sink(C, v);
     });
 }
@@ -244,7 +256,7 @@ __device__ __forceinline__ void big_inv(uint32_t (&r)[BG::R], uint32_t *buf, con
         const Lane<P> LB(opaque_lane());
         uint32_t v[32];
         source(C, v);
-        inv_pass2<P, BMIN, WIDE0>(v, tab + TW2_ENTRIES * 64 * c + opaque_zero(), lane);
+        inv_pass2<P, BMIN, WIDE0>(v, tab + BG::TS * c + opaque_zero(), lane);
         sfor<8>([&](auto Q) {
             *reinterpret_cast<uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm)) =
                 make_uint4(v[4 * Q + 0], v[4 * Q + 1], v[4 * Q + 2], v[4 * Q + 3]);
@@ -254,7 +266,7 @@ __device__ __forceinline__ void big_inv(uint32_t (&r)[BG::R], uint32_t *buf, con
         compiler_fence();
     });
     // bit-5 stage: GS with the lane-half twiddle, then swap back
-    const uint2 *sw = tab + BG::LANE_PAIRS + opaque_zero();
+    const uint2 *sw = tab + BG::SWO + opaque_zero();
     sfor<H>([&](auto Mi) {
         constexpr int m = Mi;
         const uint2 w = sw[m + H * h];
@@ -384,9 +396,12 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const
 //     store order (layout B), the complete FWD(a), one Montgomery product per
 //     coefficient, the inverse with n^-1 2^32.
 // a, b and c may alias: a wave loads its polynomial's a and b before it
-// stores any c.  BIG_MUL_WAVES transpose buffers (8 KiB each) and both
-// directions' tables (2 x 31.5 KiB) in LDS; the register phases are pinned
-// apart (pin), without which the scheduler interleaves a's forward with b's.
+// stores any c.  poly_mul_ntt: BIG_MUL_WAVES transpose buffers (8 KiB each)
+// and both directions' tables (2 x 31.5 KiB) in LDS; poly_mul (BIG_MUL_CMP):
+// 4 buffers and both compact tables (2 x 3.5 KiB), two workgroups per CU, so
+// a CU never drains to its last wave at a workgroup boundary.  The register
+// phases are pinned apart (pin), without which the scheduler interleaves a's
+// forward with b's.
 // Measured per 2^18 products (profiles/r04/f/ab_m4096.log): poly_mul 5.75 ms
 // (k_poly_mul_large) -> 4.82 (12 waves) -> 4.49 (8 waves); poly_mul_ntt
 // 4.20 -> 3.90 -> 3.67.
@@ -401,19 +416,29 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const
 #ifndef BIG_MUL
 #define BIG_MUL 1   // 0: n = 4096 products on k_poly_mul_large (A/B)
 #endif
+#ifndef BIG_MUL_CMP
+#define BIG_MUL_CMP 1   // poly_mul: compact tables (3.5 KiB per direction) on two 4-wave workgroups per CU: 4.45 -> 4.10 ms per 2^18 (profiles/r04/u)
+#endif
+template <bool BHAT>
+constexpr int big_mul_waves()
+{
+    return (!BHAT && BIG_MUL_CMP) ? 4 : BIG_MUL_WAVES;
+}
 template <int PS, bool BHAT>
-__global__ __launch_bounds__((Big<PS, BIG_MUL_WAVES>::NT), (Big<PS, BIG_MUL_WAVES>::OCC)) void k_poly_mul_big(
+using BigMul = Big<PS, big_mul_waves<BHAT>(), !BHAT && BIG_MUL_CMP>;
+template <int PS, bool BHAT>
+__global__ __launch_bounds__((BigMul<PS, BHAT>::NT), 2) void k_poly_mul_big(
     const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
 {
-    using BG = Big<PS, BIG_MUL_WAVES>;
+    using BG = BigMul<PS, BHAT>;
     using P = typename BG::P;
     using PL = typename BG::PL;
     constexpr int LOGR = mul_logr<2>();   // p-III's prime: the n = 2048 product's residues
     using BM = BaseMul<P, LOGR>;
     constexpr uint32_t N = PL::N;
-    static_assert(BG::WAVES * XPOSE_WORDS + 2 * BG::IMG_WORDS <= 160 * 256, "one workgroup per CU");
-    __shared__ __attribute__((aligned(16))) uint32_t lds[BG::WAVES * XPOSE_WORDS + 2 * BG::IMG_WORDS];
-    uint32_t *const tabfw = lds + BG::WAVES * XPOSE_WORDS, *const tabiw = tabfw + BG::IMG_WORDS;
+    static_assert(BG::WAVES * XPOSE_WORDS + 2 * BG::TAB_WORDS <= 160 * 256, "one workgroup per CU");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BG::WAVES * XPOSE_WORDS + 2 * BG::TAB_WORDS];
+    uint32_t *const tabfw = lds + BG::WAVES * XPOSE_WORDS, *const tabiw = tabfw + BG::TAB_WORDS;
     auto prologue = [&]() {
         fill_big_tw<BG, false>(tabfw);
         fill_big_tw<BG, true>(tabiw);
@@ -446,7 +471,7 @@ __global__ __launch_bounds__((Big<PS, BIG_MUL_WAVES>::NT), (Big<PS, BIG_MUL_WAVE
                         v[JP] = r[BG::creg(cc, JP)];
                         vb[JP] = rb[BG::creg(cc, JP)];
                     });
-                    BM::run(v, vb, ftab + TW2_ENTRIES * 64 * cc + opaque_zero(), lane);
+                    BM::run(v, vb, ftab + BG::TS * cc + opaque_zero(), lane);
                 },
                 c + base);
         } else {

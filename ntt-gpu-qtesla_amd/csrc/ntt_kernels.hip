@@ -218,10 +218,10 @@ template <int PS> struct LMul {
     {
         if constexpr (PS >= LARGE_PS0 && BIG_MUL && PSel<PS>::T::N == 4096) {
             // one wave per product (ntt_big.hpp)
-            using BG = Big<PS, BIG_MUL_WAVES>;
-            size_t ppw = batch / ((size_t)BG::WAVES * d.cus * 2);
+            const int waves = bhat ? big_mul_waves<true>() : big_mul_waves<false>();
+            size_t ppw = batch / ((size_t)waves * d.cus * 2);
             ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
-            const dim3 g((uint32_t)((batch + BG::WAVES * ppw - 1) / (BG::WAVES * ppw))), blk(BG::NT);
+            const dim3 g((uint32_t)((batch + waves * ppw - 1) / (waves * ppw))), blk(waves * 64);
             if (bhat) hipLaunchKernelGGL((k_poly_mul_big<PS, true>), g, blk, 0, s, a, b, c, (uint32_t)batch, (uint32_t)ppw);
             else hipLaunchKernelGGL((k_poly_mul_big<PS, false>), g, blk, 0, s, a, b, c, (uint32_t)batch, (uint32_t)ppw);
             return finish_launch();
