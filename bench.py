@@ -63,6 +63,9 @@ VALU_BOUND = {"polymul", "polymul_ntt", "nussbaumer"}
 METRIC = "NTTs/sec (fwd+inv, n=2048 qTESLA-p-III) at batch=2^20; achieved HBM GB/s"
 SEED = 0x5EED0003
 PMC_PATH = os.path.join(ROOT, "profiles", "pmc_summary.json")
+# tools-only diagnostic library (ntt-gpu-qtesla_amd/tools/ntt_diag.hip, `make tools`):
+# the transforms' memory-only variants for roofline.pattern_floor_ms
+DIAG_PATH = os.path.join(ROOT, "ntt-gpu-qtesla_amd", "lib", "libqtesla_ntt_diag.so")
 
 # BASELINE.json configs -> (op, param, batch per GPU, ring)
 CONFIGS = {
@@ -271,18 +274,65 @@ def load_valu(workload: str, batch: int, build_hash: str, kernel_key: str):
 
 def valu_roofline(v, launch_ms: float, hbm: dict) -> dict:
     """achieved = VALU issue SIMD-cycles per launch / live launch time;
-    peak = 4 SIMDs x CUs x 2.4 GHz; frac_at_held_clock uses the clock the
-    counter pass measured (GRBM_GUI_ACTIVE / 8 XCDs / kernel time)."""
+    peak = 4 SIMDs x CUs x 2.4 GHz (frac).  frac_at_held_clock is taken from
+    the counter pass ALONE: its VALU SIMD-cycles over its own cycles
+    (GRBM_GUI_ACTIVE / 8 XCDs) for the same dispatches, i.e. how busy the
+    VALU was at the clock the chip held -- never the counter pass's cycles
+    over this run's (faster, unprofiled) launch time."""
     if v is None:
         return {"bound": "valu", "achieved": None, "peak": None, "unit": "G SIMD-cycles/s", "frac": None, "hbm": hbm}
     cyc = v["valu_simd_cycles_per_launch"]
     achieved = cyc / (launch_ms * 1e-3) / 1e9
     peak = SIMDS_PER_CU * v["cus"] * PEAK_CLOCK_GHZ
-    held = SIMDS_PER_CU * v["cus"] * v["clock_ghz_pmc"]
     return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G SIMD-cycles/s", "frac": achieved / peak,
-            "frac_at_held_clock": achieved / held, "clock_ghz_pmc": v["clock_ghz_pmc"],
+            "frac_at_held_clock": v["valu_busy_at_pmc_clock"], "clock_ghz_pmc": v["clock_ghz_pmc"],
+            "held_clock_source": "counter pass: VALU SIMD-cycles / (4 SIMDs x CUs x GRBM_GUI_ACTIVE/8), same dispatches",
             "valu_insts_per_launch": v["SQ_INSTS_VALU"], "mean_simd_cycles_per_valu": v["mean_simd_cycles_per_valu"],
-            "valu_simd_cycles_per_launch": cyc, "hbm": hbm}
+            "valu_simd_cycles_per_launch": cyc, "uncosted_opcodes": v.get("uncosted_opcodes"), "hbm": hbm}
+
+
+def pattern_floor(args, ntt_amd, torch, x, stream, steps: int):
+    """The memory-only variant of the dominant transform kernels: the same
+    grid, work loop, global loads, LDS transposes and stores, no arithmetic
+    (ntt_debug_variant op 0/1 variant 3 of the tools-only diagnostic library,
+    tools/ntt_diag.hip), timed in this process AFTER the timed region on the
+    same buffer (its contents no longer matter), with an event pair around
+    `steps` back-to-back launches on the kernels' stream.  It is the access
+    pattern's own floor: kernel / floor says how much the arithmetic costs
+    the memory stream.  Never part of `value`."""
+    import ctypes
+    if args.op not in ("fwdinv", "fwd", "inv") or ntt_amd.param_info(args.param)["n"] > 2048:
+        return None
+    if not os.path.exists(DIAG_PATH):
+        return {"note": f"{os.path.relpath(DIAG_PATH, ROOT)} not built (make -C ntt-gpu-qtesla_amd tools)"}
+    L = ctypes.CDLL(DIAG_PATH)
+    vp = ctypes.c_void_p
+    L.ntt_debug_variant.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
+    ps = ntt_amd.PARAM_SETS[args.param]
+    npoly = x.numel() // ntt_amd.param_info(args.param)["n"]
+    kinds = {"fwdinv": ["fwd", "inv"], "fwd": ["fwd"], "inv": ["inv"]}[args.op]
+    sp = vp(stream.cuda_stream)
+    ms = {}
+    for k in kinds:
+        op = 0 if k == "fwd" else 1
+
+        def run():
+            rc = L.ntt_debug_variant(op, 3, vp(x.data_ptr()), vp(x.data_ptr()), npoly, ps, sp)
+            if rc != 0:
+                raise RuntimeError(f"ntt_debug_variant({op}, 3) failed: {rc}")
+        for _ in range(2):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(x.device)
+        e0.record(stream)
+        for _ in range(steps):
+            run()
+        e1.record(stream)
+        torch.cuda.synchronize(x.device)
+        ms[k] = e0.elapsed_time(e1) / steps
+    return {"ms": ms, "steps": steps,
+            "kernel": "k_variant<PS, INV, 3> (tools/ntt_diag.hip: loads + LDS transpose + stores, no arithmetic)",
+            "timing": "region events / steps, after the timed region"}
 
 
 def workload_name(op, param, n, q, ring):
@@ -316,6 +366,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-floor", action="store_true", help="skip roofline.pattern_floor_ms (transforms)")
     args = ap.parse_args()
     c_op, c_param, c_batch, c_ring = CONFIGS[args.config]
     args.op = args.op or c_op
@@ -436,6 +487,7 @@ def main():
         check["all_ranks_ok"] = dist.max(bad) == 0.0
     if expiries is not None:
         check["slot_sync_expiries"] = expiries
+    floor = None if args.no_floor else pattern_floor(args, ntt_amd, torch, x, stream, max(args.steps, 10))
 
     units = world * count * args.steps
     value = units / elapsed
@@ -447,6 +499,12 @@ def main():
            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
            "avg_launch_ms": per_kind[dom], "alg_bytes_per_launch": alg_bytes,
            "timing": "region events / steps" if single else "per-launch events", "per_kernel_ms": per_kind}
+    if floor is not None:
+        hbm["pattern_floor"] = floor
+        if dom in floor.get("ms", {}):
+            hbm["pattern_floor_ms"] = floor["ms"][dom]
+            hbm["kernel_over_floor"] = per_kind[dom] / floor["ms"][dom]
+            hbm["floor_frac"] = alg_bytes / (floor["ms"][dom] * 1e-3) / 1e9 / HBM_PEAK_GBS
     if args.op in VALU_BOUND:
         v, v_note = load_valu(workload, count, build_hash, dom)
         roofline = dict(valu_roofline(v, per_kind[dom], hbm), kernel=dom, valu_note=v_note,

@@ -92,6 +92,7 @@ struct Big {
     // CMP (the products' incomplete domain): per chunk only lane entries
     // 0 .. MUL_CENT-1, then the bit-5 pairs -- TS pairs per chunk, the bit-5
     // pairs at SWO, TAB_WORDS per direction
+    static constexpr bool CMP_ = CMP;
     static constexpr int TS = CMP ? MUL_CENT * 64 : TW2_ENTRIES * 64;
     static constexpr int SWO = CMP ? CH * TS : LANE_PAIRS;
     static constexpr int TAB_WORDS = CMP ? 2 * (CH * TS + R) : IMG_WORDS;
@@ -397,35 +398,26 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const
 //     coefficient, the inverse with n^-1 2^32.
 // a, b and c may alias: a wave loads its polynomial's a and b before it
 // stores any c.  poly_mul_ntt: BIG_MUL_WAVES transpose buffers (8 KiB each)
-// and both directions' tables (2 x 31.5 KiB) in LDS; poly_mul (BIG_MUL_CMP):
-// 4 buffers and both compact tables (2 x 3.5 KiB), two workgroups per CU, so
-// a CU never drains to its last wave at a workgroup boundary.  The register
-// phases are pinned apart (pin), without which the scheduler interleaves a's
-// forward with b's.
+// and both directions' tables (2 x 31.5 KiB) in LDS; poly_mul: 4 buffers and
+// both compact tables (2 x 3.5 KiB), two workgroups per CU, so a CU never
+// drains to its last wave at a workgroup boundary (4.45 -> 4.10 ms per 2^18,
+// profiles/r04/u).  The register phases are pinned apart (pin), without which
+// the scheduler interleaves a's forward with b's.  b-hat's loads are issued
+// before a's forward (poly_mul_ntt 3.64 -> 3.55 ms), b's are not (poly_mul
+// 4.24 -> 4.39 when they are, profiles/r04/g/ab_m4096.log).
 // Measured per 2^18 products (profiles/r04/f/ab_m4096.log): poly_mul 5.75 ms
-// (k_poly_mul_large) -> 4.82 (12 waves) -> 4.49 (8 waves); poly_mul_ntt
-// 4.20 -> 3.90 -> 3.67.
+// (the multi-wave k_poly_mul_large) -> 4.82 (12 waves) -> 4.49 (8 waves);
+// poly_mul_ntt 4.20 -> 3.90 -> 3.67.
 #ifndef BIG_MUL_WAVES
 #define BIG_MUL_WAVES 8   // 2 per SIMD, 0 spills (12 waves = 3 per SIMD: 27 VGPRs spilled, 7 % slower)
-#endif
-#ifndef BIG_MUL_PF
-// b's loads issued before a's forward: poly_mul_ntt 3.64 -> 3.55 ms, poly_mul
-// 4.24 -> 4.39 (profiles/r04/g/ab_m4096.log), so b-hat only
-#define BIG_MUL_PF BHAT
-#endif
-#ifndef BIG_MUL
-#define BIG_MUL 1   // 0: n = 4096 products on k_poly_mul_large (A/B)
-#endif
-#ifndef BIG_MUL_CMP
-#define BIG_MUL_CMP 1   // poly_mul: compact tables (3.5 KiB per direction) on two 4-wave workgroups per CU: 4.45 -> 4.10 ms per 2^18 (profiles/r04/u)
 #endif
 template <bool BHAT>
 constexpr int big_mul_waves()
 {
-    return (!BHAT && BIG_MUL_CMP) ? 4 : BIG_MUL_WAVES;
+    return !BHAT ? 4 : BIG_MUL_WAVES;
 }
 template <int PS, bool BHAT>
-using BigMul = Big<PS, big_mul_waves<BHAT>(), !BHAT && BIG_MUL_CMP>;
+using BigMul = Big<PS, big_mul_waves<BHAT>(), !BHAT>;
 template <int PS, bool BHAT>
 __global__ __launch_bounds__((BigMul<PS, BHAT>::NT), 2) void k_poly_mul_big(
     const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
@@ -435,6 +427,7 @@ __global__ __launch_bounds__((BigMul<PS, BHAT>::NT), 2) void k_poly_mul_big(
     using PL = typename BG::PL;
     constexpr int LOGR = mul_logr<2>();   // p-III's prime: the n = 2048 product's residues
     using BM = BaseMul<P, LOGR>;
+    static_assert(!BG::CMP_ || MUL_CENT >= (1 << (5 - LOGR)) - 1, "the compact table holds every lane entry pass 2 reads");
     constexpr uint32_t N = PL::N;
     static_assert(BG::WAVES * XPOSE_WORDS + 2 * BG::TAB_WORDS <= 160 * 256, "one workgroup per CU");
     __shared__ __attribute__((aligned(16))) uint32_t lds[BG::WAVES * XPOSE_WORDS + 2 * BG::TAB_WORDS];
@@ -456,10 +449,9 @@ __global__ __launch_bounds__((BigMul<PS, BHAT>::NT), 2) void k_poly_mul_big(
         };
         uint32_t rb[BG::R];
         if constexpr (!BHAT) {
-            if constexpr (BIG_MUL_PF) big_load_a<BG>(rb, b + base, lane);
             big_fwd<BG, LOGR>(r, buf, ftab, h, lane, keep(r));
             pin(r);   // phase boundary: nothing of b's forward moves above it
-            if constexpr (!BIG_MUL_PF) big_load_a<BG>(rb, b + base, lane);   // 64 fewer live VGPRs through a's forward
+            big_load_a<BG>(rb, b + base, lane);   // 64 fewer live VGPRs through a's forward
             big_fwd<BG, LOGR>(rb, buf, ftab, h, lane, keep(rb));
             pin(rb);
             big_inv<BG, LOGR, BM::WIDE, PL::template ninv_r<LOGR>(), PL::template c1_r<LOGR>()>(
@@ -475,10 +467,9 @@ __global__ __launch_bounds__((BigMul<PS, BHAT>::NT), 2) void k_poly_mul_big(
                 },
                 c + base);
         } else {
-            if constexpr (BIG_MUL_PF) big_load_b<BG>(rb, b + base, lane);
+            big_load_b<BG>(rb, b + base, lane);   // b-hat in the forward's store order, before a's forward
             big_fwd<BG, 0>(r, buf, ftab, h, lane, keep(r));
             pin(r);
-            if constexpr (!BIG_MUL_PF) big_load_b<BG>(rb, b + base, lane);   // b-hat in the forward's store order
             big_inv<BG, 0, false, PL::NINV_R, PL::C1_R>(
                 r, buf, itab, h, lane,
                 [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {

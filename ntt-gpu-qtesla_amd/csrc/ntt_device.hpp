@@ -399,7 +399,7 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
     fwd_pass1_tw<P>(r, h, tw_base<PS, false>(), sw);
 }
 
-// ---- typed forward for poly_mul (MUL_LAZYBIAS) ---------------------------
+// ---- typed forward for poly_mul --------------------------------------------
 // Inside the fused product the forward's outputs never leave the kernel, so a
 // butterfly may skip the +2q bias of y' = a - t + 2q when the value's next
 // consumer tolerates a signed value in (-2q, 2q) ("S" type; "U" = [0, 4q)):
@@ -410,10 +410,10 @@ __device__ __forceinline__ void fwd_pass1(uint32_t (&r)[32], uint32_t h, const u
 // stage s <= 3 is S iff it was the y output).  Pass 1's S-typed multiplies
 // use the centred twiddles below (compile-time literals, k < 32); pass 2's
 // lane twiddles exist unsigned only, so there a y' is left S only when its
-// consumer is an x input or BaseMul.
-#ifndef MUL_LAZYBIAS
-#define MUL_LAZYBIAS 1   // with MUL_HOIST: -1.4 % (p-III) / -2.2 % (p-I); alone +1.5 % / +0.9 % (profiles/r03/ab_polymul_*.log)
-#endif
+// consumer is an x input or BaseMul.  With the loop-invariant transpose
+// addresses it pays for: -1.4 % (p-III) / -2.2 % (p-I); alone +1.5 % / +0.9 %
+// (profiles/r03/ab_polymul_*.log).  In poly_ntt (HBM-bound) it was -0.6 %
+// p-III, 0 p-I (profiles/r03/ab_fwd_lazybias.log) and is not used there.
 __host__ __device__ constexpr uint32_t cbrv32(uint32_t x, int bits)
 {
     uint32_t r = 0;
@@ -536,7 +536,7 @@ __device__ __forceinline__ void fwd_pass2(uint32_t (&r)[32], const uint2 *tab, u
 }
 
 // WIDE0: the first stage's inputs lie in [0, 3q) with |x - y| < 2^31
-// (poly_mul's BaseMul with a half-canonical first operand, MUL_AHALF, p-III:
+// (poly_mul's BaseMul with a half-canonical first operand, p-III:
 // [0, 2.19q)): x' = (x + y) mod 2q by a three-candidate min (v_min3)
 template <class P, int BMIN = 0, bool WIDE0 = false>
 __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, uint32_t lane)
@@ -573,43 +573,25 @@ __device__ __forceinline__ void inv_pass2(uint32_t (&r)[32], const uint2 *tab, u
 // final scaling with (n/D)^-1); outputs above 2q get one conditional
 // subtraction.  Replaces LOGR stages of each forward and of the inverse and
 // the pointwise product.
-#ifndef NTT_FWD_LZ
-#define NTT_FWD_LZ 0   // A/B switch: poly_ntt with the typed lazy-bias passes (HBM-bound: -0.6 % p-III, 0 p-I, profiles/r03/ab_fwd_lazybias.log)
-#endif
-#ifndef MUL_HOIST
-// poly_mul's transposes with loop-invariant lane addresses instead of the
-// per-transpose recomputation from an opaque lane (which kept the r02 kernel
-// from spilling): affordable once MUL_LAZYBIAS took the p-III kernel from 126
-// to 96 VGPRs (121 with the hoisted addresses, no spills)
-#define MUL_HOIST 1
-#endif
-#ifndef MUL_ZSPLIT
-#define MUL_ZSPLIT 1
-#endif
-#ifndef MUL_AHALF
-#define MUL_AHALF 1   // p-III poly_mul -1.3 % (profiles/r03/ab_polymul_ahalf.log)
-#endif
 template <class P, int LOGR>
 struct BaseMul {
     static constexpr int D = 1 << LOGR;
+    static_assert(D >= 2, "the zeta-split residue products need D >= 2");
     static constexpr double QD = P::Q;
-    static_assert(D * QD * QD + 4294967296.0 * QD < 18446744073709551616.0, "REDC input fits 64 bits");
-    // REDC output bound D q^2 / 2^32 + q: below 2q, or below 4q with a csub
-    static constexpr bool OUT_CSUB = D * QD * QD / 4294967296.0 + QD >= 2.0 * QD;
-    static_assert(D * QD * QD / 4294967296.0 + QD < 4.0 * QD, "one conditional subtraction reaches [0, 2q)");
     static constexpr int E0 = (1 << (4 - LOGR)) - 1;   // LDS entry of the stage on pos bit LOGR
 
-    // zeta-split form (MUL_ZSPLIT): c_k = L_k + zeta R * REDC(H_k), L_k / H_k the
+    // zeta-split form: c_k = L_k + zeta R * REDC(H_k), L_k / H_k the
     // sums of the D products without / with the wrap (a, b canonical, H_k
     // < (D-1) q^2), zeta R = zeta 2^32 mod q in [0, q] per residue PAIR (the
     // +w / -w residues share w).  Per residue that is 7 x (REDC + one 64-bit
-    // multiply-add) instead of 7 b~ products (Shoup + two-candidate min).
+    // multiply-add) instead of 7 b~ products (Shoup + two-candidate min):
+    // p-III 8.19 -> 8.04 ms, p-I 3.65 -> 3.58 ms (profiles/r03/ab_polymul_zsplit_lz.log).
     // Bound: c_k < (k+1) q^2 + q ((D-1-k) q^2 / 2^32 + q) <= (D + q/2^32) q^2.
     static constexpr double CZ = (D + QD / 4294967296.0) * QD * QD;
     static_assert(CZ + 4294967296.0 * QD < 18446744073709551616.0, "zeta-split REDC input fits 64 bits");
     static_assert(CZ / 4294967296.0 + QD < 4.0 * QD, "zeta-split: one conditional subtraction reaches [0, 2q)");
     static constexpr bool OUT_CSUB_Z = CZ / 4294967296.0 + QD >= 2.0 * QD;
-    // MUL_AHALF: a only reduced to [0, 2q) (one conditional subtraction
+    // Half-canonical a: a only reduced to [0, 2q) (one conditional subtraction
     // instead of two), b canonical: c_k < 2 D q^2 (the k = D-1 sum; the others
     // stay below (2D - 1 + 2q/2^32) q^2).  The REDC output may then pass 4q
     // (p-III: 4.19q): one conditional subtraction leaves it below WH = 2.19q and
@@ -618,12 +600,13 @@ struct BaseMul {
     static_assert(CZH + 4294967296.0 * QD < 18446744073709551616.0, "half-canonical REDC input fits 64 bits");
     static constexpr double OUTH = CZH / 4294967296.0 + QD;
     static constexpr double WH = OUTH >= 2.0 * QD ? OUTH - 2.0 * QD : OUTH;   // after the csub
-    static_assert(!(MUL_AHALF && OUT_CSUB_Z) || (WH < 3.0 * QD && WH < 2147483648.0 && 2.0 * WH < 4294967296.0),
+    static_assert(!OUT_CSUB_Z || (WH < 3.0 * QD && WH < 2147483648.0 && 2.0 * WH < 4294967296.0),
                   "first inverse stage: x + y < 6q fits 32 bits, |x - y| < 2^31");
     static constexpr bool OUT_CSUB_H = OUTH >= 2.0 * QD;
     // only where the z-split output already needs its conditional subtraction
-    // (p-III); elsewhere the half-canonical a would move one csub to the output
-    static constexpr bool AH = MUL_AHALF && OUT_CSUB_Z;
+    // (p-III, -1.3 %, profiles/r03/ab_polymul_ahalf.log); elsewhere the
+    // half-canonical a would move one csub to the output
+    static constexpr bool AH = OUT_CSUB_Z;
     static constexpr bool WIDE = AH && OUTH >= 4.0 * QD;   // inverse's first stage in WIDE0 form
 
     static __device__ __forceinline__ uint32_t redc(uint64_t c)
@@ -632,7 +615,7 @@ struct BaseMul {
         return (uint32_t)(((uint64_t)m * P::Q + c) >> 32);
     }
 
-    // [0,4q) (U) or (-2q,2q) (S, MUL_LAZYBIAS) -> canonical [0,q)
+    // [0,4q) (U) or (-2q,2q) (S, typed forward) -> canonical [0,q)
     // (s is a compile-time constant once the residue loop is unrolled)
     static __device__ __forceinline__ uint32_t canon(bool s, uint32_t x)
     {
@@ -688,38 +671,7 @@ struct BaseMul {
     template <bool ODD_S = false>
     static __device__ __forceinline__ void run(uint32_t (&ra)[32], const uint32_t (&rb)[32], const uint2 *tab, uint32_t lane)
     {
-#if MUL_ZSPLIT
-        if constexpr (D >= 2) {
-            run_zsplit<ODD_S>(ra, rb, tab, lane);
-            return;
-        }
-#endif
-#pragma unroll
-        for (int g = 0; g < 32 / D; ++g) {
-            const uint2 w = tab[tw2_idx<P>(E0 + (g >> 1), lane)];   // (-w mod 2^32, w')
-            uint32_t a[D], b[D], bt[D];
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                a[i] = canon(ODD_S && (g & 1), ra[D * g + i]);
-                b[i] = canon(ODD_S && (g & 1), rb[D * g + i]);
-            }
-#pragma unroll
-            for (int i = 1; i < D; ++i) {
-                const uint32_t y = b[i];
-                const uint32_t tn = madlo32(__umulhi(y, w.y), P::Q, y * w.x);   // -(b w mod q), in (-2q, 0]
-                // zeta b_i in [0, q]: +w -> min(-tn, -tn - q); -w -> min(tn + q, tn + 2q)
-                bt[i] = (g & 1) ? umin(tn + P::Q, tn + P::Q2) : umin(0u - tn, (0u - P::Q) - tn);
-            }
-#pragma unroll
-            for (int k = 0; k < D; ++k) {
-                uint64_t c = 0;
-#pragma unroll
-                for (int i = 0; i < D; ++i) c += (uint64_t)a[i] * (i <= k ? b[k - i] : bt[k + D - i]);
-                const uint32_t m = (uint32_t)c * P::QNEG;
-                const uint32_t r = (uint32_t)(((uint64_t)m * P::Q + c) >> 32);
-                ra[D * g + k] = OUT_CSUB ? csub<P::Q2>(r) : r;
-            }
-        }
+        run_zsplit<ODD_S>(ra, rb, tab, lane);
     }
 };
 
@@ -852,15 +804,10 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
 // incomplete-domain product and the per-transpose address recomputation
 // (fresh lanes) brought it under 128 VGPRs: 4 waves/SIMD is 4 % faster there
 // (poly_mul_ntt 8 %), profiles/r02/ab_polymul_incomplete.log
-// poly_mul's residue degree 2^LOGR: 8 (3 stages of each transform replaced
-// by 8x8 products) is 3 % faster than 4 on p-III and 6 % on p-I; 16 spills
-// (profiles/r02/ab_polymul_incomplete.log)
-#ifndef MUL_LOGR
-#define MUL_LOGR 3
-#endif
-#ifndef MUL_LOGR_SMALL
-#define MUL_LOGR_SMALL MUL_LOGR
-#endif
+// poly_mul's residue degree 2^MUL_LOGR: 8 (3 stages of each transform
+// replaced by 8x8 products) is 3 % faster than 4 on p-III and 6 % on p-I; 16
+// spills (profiles/r02/ab_polymul_incomplete.log)
+constexpr int MUL_LOGR = 3;
 #ifndef MUL_WG
 #define MUL_WG 1024
 #endif
@@ -870,22 +817,21 @@ __device__ __forceinline__ void chunk_loop(uint32_t nunits, uint32_t ppw, Prolog
 #ifndef MUL_WAVES_PER_SIMD
 #define MUL_WAVES_PER_SIMD 4
 #endif
-// MUL_COMPACT: poly_mul (not poly_mul_ntt) reads only lane-table entries
+// Compact tables: poly_mul (not poly_mul_ntt) reads only lane-table entries
 // 0..2 (pass 2 stops at pos bit 3; BaseMul's zeta are entries 1, 2) and the
 // bit-5 pairs, so its workgroup keeps just those (compact tables: 3.5 KiB for
 // both directions instead of 31.5) and runs as two 8-wave workgroups per CU
 // (same 4 waves/SIMD): the CU no longer drains to start the next workgroup.
 // p-III 7.69 -> 7.35 ms, p-I 3.46 -> 3.25 ms per 2^20 (profiles/r04/r/)
-#ifndef MUL_COMPACT
-#define MUL_COMPACT 1
-#endif
-template <int PS, bool BHAT> constexpr bool mul_compact() { return MUL_COMPACT && !BHAT; }
+template <int PS, bool BHAT> constexpr bool mul_compact() { return !BHAT; }
 template <int PS, bool BHAT = false> constexpr int mul_wg() { return mul_compact<PS, BHAT>() ? 512 : MUL_WG; }
 template <int PS> constexpr int mul_occ() { return MUL_WAVES_PER_SIMD; }
-constexpr int MUL_CENT = 3;   // lane-table entries a compact table keeps
+// lane-table entries a compact table keeps: the stages on pos bits 4 .. LOGR
+// read entries 0 .. 2^(5-LOGR) - 2, BaseMul's zeta the last 2^(4-LOGR) of them
+constexpr int MUL_CENT = (1 << (5 - MUL_LOGR)) - 1;
 // compact table image: entries 0..MUL_CENT-1 (L lanes each), then the 32 bit-5 pairs
 template <class P> constexpr int mul_ctab_words() { return MUL_CENT * (int)tw2_lanes<P>() * 2 + 64; }
-template <int PS> constexpr int mul_logr() { return PSel<PS>::T::LOGN == 11 ? MUL_LOGR : MUL_LOGR_SMALL; }
+template <int PS> constexpr int mul_logr() { return MUL_LOGR; }
 constexpr int WG = 256;   // elementwise kernels
 constexpr int NTT_WAVES = NTT_WG / 64;
 constexpr int NTT_LDS_WORDS = NTT_WAVES * XPOSE_WORDS + TW2_WORDS;
@@ -913,9 +859,6 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
     };
     // canonical output: BR=false from the bit-reversed pass-2 registers to
     // natural order, brv5(j)*S + lane; BR=true from the pass-1 arrangement
-    // NTT_FWD_LZ: the typed lazy-bias passes of poly_mul (fwd_pass1_lz /
-    // fwd_pass2_lz down to bit 0: odd registers end in S form)
-    constexpr bool LZ = NTT_FWD_LZ && !BR;
     auto store = [&](uint32_t (&r)[32], uint32_t u) {
         const uint32_t poly = L.poly(u);
         if (LT::BIG || poly < npoly) {
@@ -923,14 +866,12 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
             if constexpr (BR) dst += LT::BIG ? 32 * L.h : 0u;   // brl + 32 h = l5 + 64 h (p1s_off)
 #pragma unroll
             for (int j = 0; j < 32; ++j) {
-                const uint32_t v = (LZ && (j & 1)) ? csub<P::Q>(umin(r[j], r[j] + P::Q2)) : canon4<P>(r[j]);
-                st_out(dst + (BR ? p1s_off<P>(j) : brv5(j) * LT::S), v);
+                st_out(dst + (BR ? p1s_off<P>(j) : brv5(j) * LT::S), canon4<P>(r[j]));
             }
         }
     };
     auto front = [&](uint32_t (&r)[32], uint32_t) {
-        if constexpr (LZ) fwd_pass1_lz<P>(r, L.h, tw_base<PS, false>(), tw2 + TW2_ENTRIES * 64 + opaque_zero());
-        else fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
+        fwd_pass1<PS, P>(r, L.h, tw2 + TW2_ENTRIES * 64 + opaque_zero());
         lds_p1_to_p2<P>(r, buf, L);
         if constexpr (BR) {
             fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
@@ -938,8 +879,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_ntt_fwd(const ui
         }
     };
     auto back = [&](uint32_t (&r)[32], uint32_t u) {
-        if constexpr (LZ) fwd_pass2_lz<P, 0>(r, tw2 + opaque_zero(), L.lane);
-        else if constexpr (!BR) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
+        if constexpr (!BR) fwd_pass2<P>(r, tw2 + opaque_zero(), L.lane);
         store(r, u);
     };
     auto process = [&](uint32_t (&r)[32], uint32_t u) {
@@ -1035,7 +975,7 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_bitrev(const uin
 // VAR (tools/ntt_diag.hip only, bottleneck attribution): 1 = global loads
 // and stores only (no arithmetic, no LDS), 2 = arithmetic + LDS only
 // (register-made inputs, outputs kept live, nothing stored).
-// compact copy of a direction's image (MUL_COMPACT)
+// compact copy of a direction's image (mul_compact)
 template <int PS, bool INV, int NT>
 __device__ __forceinline__ void fill_tw2_compact(uint2 *tab)
 {
@@ -1052,6 +992,7 @@ __global__ __launch_bounds__((mul_wg<PS, BHAT>()), mul_occ<PS>()) void k_poly_mu
     using P = typename PSel<PS>::T;
     using LT = Lane<P>;
     constexpr bool CMP = mul_compact<PS, BHAT>();
+    static_assert(MUL_CENT >= (1 << (5 - mul_logr<PS>())) - 1, "the compact table holds every lane entry pass 2 reads");
     constexpr int WG_ = mul_wg<PS, BHAT>();
     constexpr int WAVES = WG_ / 64;
     constexpr int TABW = CMP ? mul_ctab_words<P>() : TW2_WORDS;   // words per direction
@@ -1100,12 +1041,15 @@ __global__ __launch_bounds__((mul_wg<PS, BHAT>()), mul_occ<PS>()) void k_poly_mu
                 if (valid) st_out(pc + LT::S * j, ra[j] + rb[j]);
             continue;
         }
-        constexpr bool LZ = !BHAT && MUL_LAZYBIAS;   // typed forwards (fwd_pass1_lz)
+        constexpr bool LZ = !BHAT;   // typed forwards (fwd_pass1_lz)
         if constexpr (LZ) fwd_pass1_lz<P>(ra, L.h, tw_base<PS, false>(), ftw2 + SWO + opaque_zero());
         else fwd_pass1<PS, P>(ra, L.h, ftw2 + SWO + opaque_zero());
-        // b-hat product: n = 2048 keeps the hoisted addresses, n = 1024 (32-lane
-        // twiddle table) recomputes them (hoisted: 22 spilled VGPRs)
-        constexpr bool HOIST = BHAT ? P::LOGN == 11 : MUL_HOIST;
+        // loop-invariant transpose addresses (poly_mul: affordable once the
+        // typed forwards took the p-III kernel from 126 to 96 VGPRs, 121 with
+        // the hoisted addresses, no spills); the b-hat product keeps them at
+        // n = 2048 and recomputes them from an opaque lane at n = 1024 (32-lane
+        // twiddle table; hoisted: 22 spilled VGPRs)
+        constexpr bool HOIST = BHAT ? P::LOGN == 11 : true;
         lds_p1_to_p2<P>(ra, buf, HOIST ? L : LT(opaque_lane()));
         if constexpr (LZ) fwd_pass2_lz<P, mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
         else fwd_pass2<P, BHAT ? 0 : mul_logr<PS>()>(ra, ftw2 + opaque_zero(), L.lane);
@@ -1128,12 +1072,12 @@ __global__ __launch_bounds__((mul_wg<PS, BHAT>()), mul_occ<PS>()) void k_poly_mu
             // LOGR (BaseMul)
             if constexpr (LZ) fwd_pass1_lz<P>(rb, L.h, tw_base<PS, false>(), ftw2 + SWO + opaque_zero());
             else fwd_pass1<PS, P>(rb, L.h, ftw2 + SWO + opaque_zero());
-            lds_p1_to_p2<P>(rb, buf, MUL_HOIST ? L : LT(opaque_lane()));
+            lds_p1_to_p2<P>(rb, buf, L);
             if constexpr (LZ) fwd_pass2_lz<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
             else fwd_pass2<P, mul_logr<PS>()>(rb, ftw2 + opaque_zero(), L.lane);
             BaseMul<P, mul_logr<PS>()>::template run<LZ>(ra, rb, ftw2 + opaque_zero(), L.lane);
             inv_pass2<P, mul_logr<PS>(), BaseMul<P, mul_logr<PS>()>::WIDE>(ra, itw2 + opaque_zero(), L.lane);
-            lds_p2_to_p1<P>(ra, buf, MUL_HOIST ? L : LT(opaque_lane()));
+            lds_p2_to_p1<P>(ra, buf, L);
             inv_pass1<PS, P, P::template ninv_r<mul_logr<PS>()>(), P::template c1_r<mul_logr<PS>()>()>(ra, L.h, itw2 + SWO + opaque_zero(), emit);
         } else {
 #pragma unroll

@@ -216,7 +216,7 @@ template <int PS> struct LMul {
     static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s, bool bhat,
                    const DevInfo &d)
     {
-        if constexpr (PS >= LARGE_PS0 && BIG_MUL && PSel<PS>::T::N == 4096) {
+        if constexpr (PS >= LARGE_PS0 && PSel<PS>::T::N == 4096) {
             // one wave per product (ntt_big.hpp)
             const int waves = bhat ? big_mul_waves<true>() : big_mul_waves<false>();
             size_t ppw = batch / ((size_t)waves * d.cus * 2);
@@ -453,7 +453,7 @@ int ntt_build_info(char *buf, size_t len)
         "qtesla_ntt gfx950: 1 launch/op, wave-per-poly (n=2048) / half-wave-per-poly (n=1024), 32 coeff/lane, "
         "LDS XOR-swizzled transpose, permlane32 bit-5 stage, Shoup/Harvey lazy CT + signed-Shoup GS butterflies, "
         "dispatch-ordered unit chunks; wg=" QNTT_STR(NTT_WG)
-        " mul_wg=" QNTT_STR(MUL_WG) " mul_compact=" QNTT_STR(MUL_COMPACT) " ppw<=" QNTT_STR(NTT_PPW_MAX)
+        " mul_wg=" QNTT_STR(MUL_WG) " mul_compact=1 ppw<=" QNTT_STR(NTT_PPW_MAX)
         " min_wg/cu=" QNTT_STR(NTT_MIN_WG_PER_CU) "; src=" QNTT_SRC_HASH;
     const int n = (int)strlen(s);
     if (!buf || !len) return n;

@@ -12,8 +12,8 @@
 // bits L-1 .. 0 (L = log2 n):
 //   * the first g = log2 G stages (pos bits L-1 .. 11) pair sub-block B with
 //     sub-block B ^ 2^(g-1-s): in registers from chunked loads plus one LDS
-//     exchange (the in-register head, LARGE_HEAD), or radix-2 stages ACROSS
-//     waves, one LDS exchange round each (cross_ct / cross_gs);
+//     exchange (the in-register head; rounds 2-3 ran them as radix-2 stages
+//     across waves, one LDS exchange round each, 6-8.5 % slower);
 //   * sub-block B is then a 2048-point transform whose twiddles are its own
 //     sub-tree of the n-point table, T_B[2^s + m] = psi^brv(2^s (2^g + B) + m):
 //     the n = 2048 kernel's passes (register pass, permlane32 stage, LDS
@@ -61,45 +61,39 @@ __constant__ uint2 c_fscale[LARGE_NPS][2][LARGE_GMAX][32];
 
 constexpr int TW2_BIT5_VEC4 = TW2_ENTRIES * 64 * 2 / 4;   // uint4 offset of the bit-5 table in an image
 
-template <int PS, int MULW = 0, bool INC_ = false, bool BIT5U_ = false>
+// The fused products hold one operand's 32 transformed words through the
+// other's transform, both directions' tables in LDS.  Two table forms:
+//   INC (poly_mul, the incomplete domain: residues mod x^8 -+ zeta, the
+//     n = 2048 product's BaseMul): pass 2 stops at pos bit 3, so a sub-tree's
+//     lane table is only its first MUL_CENT entries (+ its bit-5 table) and
+//     every B keeps its own (no shared table, no sub-tree scaling);
+//   shared (poly_mul_ntt, b-hat in the full domain): the sub-trees share T_0's
+//     lane table and scale by c_fscale (one 15.5 KiB image per direction
+//     instead of four: 16 waves per workgroup instead of 12, transforms
+//     4.94 / 4.75 -> 4.62 / 4.59 ms per 2^18 polys, profiles/r03/ab_l*_tab.log),
+//     and take their bit-5 pairs from __constant__ memory (c_bit5L, a
+//     per-lane select of two scalar-loaded candidates), which leaves room for
+//     16 waves at 4 per SIMD (4.37 -> 4.19 ms per 2^17, profiles/r04/n).
+template <int PS, int MULW, bool INC_>
 struct Large {
     using PL = typename PSel<PS>::T;   // the n-point set
     using P = PS2;                     // 2048-point sub-transforms over the same prime
     static_assert(PL::Q == P::Q, "large-n sets use p-III's prime");
     static constexpr int G = (int)(PL::N / 2048);
     static constexpr int LOGG = G == 2 ? 1 : 2;
-    // One workgroup per CU at 4 waves per SIMD: 16 waves x 8 KiB + the
-    // twiddle tables.  n = 4096: both sub-tree tables (2 x 15.75 KiB);
-    // n = 8192: four would only leave room for 12 waves, so the sub-trees
-    // share T_0's lane table and scale by c_fscale (SHARED): 4.94 / 4.75 ->
-    // 4.62 / 4.59 ms fwd / inv per 2^18 polys, while at n = 4096 the scaling
-    // only costs (3.98 / 3.97 -> 4.20 / 4.04 ms), profiles/r03/ab_l*_tab.log
-    // The fused products (MULW = their waves per workgroup) hold one
-    // operand's 32 transformed words through the other's transform: 12 waves
-    // at 3 per SIMD (168 VGPRs) or 8 at 2 (256), both directions' tables in
-    // LDS, always the shared lane table.
-    static constexpr bool MUL = MULW != 0;
-    static constexpr int WAVES = MUL ? MULW : 16;
-    // INC: poly_mul in the incomplete domain (residues mod x^8 -+ zeta, the
-    // n = 2048 product's BaseMul): pass 2 stops at pos bit 3, so a sub-tree's
-    // lane table is only its first three entries (+ its bit-5 table) and every
-    // B keeps its own (no shared table, no sub-tree scaling)
+    static constexpr int WAVES = MULW;
     static constexpr bool INC = INC_;
-    static constexpr int INC_ENTRIES = 3;
+    static constexpr int INC_ENTRIES = MUL_CENT;
+    static_assert(!INC || INC_ENTRIES >= (1 << (5 - MUL_LOGR)) - 1, "the compact table holds every lane entry pass 2 reads");
     static constexpr int CTAB_WORDS = INC_ENTRIES * 64 * 2 + 64;   // compact per-B image
-    static constexpr bool SHARED = !INC && (MUL || G == 4);
+    static constexpr bool SHARED = !INC;
+    static constexpr bool BIT5U = !INC;
     static constexpr int OCC = WAVES / 4;
     static constexpr int SLOTS = WAVES / G;   // polynomials per workgroup step
     static constexpr int NT = WAVES * 64;
     static constexpr int IDX = PS - LARGE_PS0;
-    // lane tables (shared: T_0's + per-B bit-5 tables; else G whole images)
-    // BIT5U: the sub-trees' bit-5 pairs from __constant__ memory (c_bit5L,
-    // per-lane select of two scalar-loaded candidates) instead of LDS: the
-    // shared table alone then leaves room for 16 waves
-    static constexpr bool BIT5U = BIT5U_;
-    static_assert(!BIT5U || (SHARED && !INC), "BIT5U: shared-table kernels only");
-    static constexpr int TAB_WORDS = INC ? G * CTAB_WORDS : SHARED ? (BIT5U ? TW2_BIT5_VEC4 * 4 : TW2_WORDS + G * 64) : G * TW2_WORDS;
-    static constexpr int NTAB = MUL ? 2 : 1;   // forward table, then (MUL) the inverse's
+    static constexpr int TAB_WORDS = INC ? G * CTAB_WORDS : TW2_BIT5_VEC4 * 4;
+    static constexpr int NTAB = 2;   // forward table, then the inverse's
     static constexpr int LDS_WORDS = WAVES * XPOSE_WORDS + NTAB * TAB_WORDS + SLOTS + 1;   // + slot counters, poison word
 };
 
@@ -128,9 +122,6 @@ __host__ __device__ constexpr uint32_t brv_g(uint32_t b, int logg) { return logg
 // requests of one wave are served in order, so it sees the poison too.  The
 // expiry is also counted on the device (ntt_sync_expiries; bench.py fails a
 // run whose count is not 0).
-#ifndef LARGE_SLOT_SYNC
-#define LARGE_SLOT_SYNC 1
-#endif
 #ifndef LARGE_SLOT_SYNC_SPIN
 #define LARGE_SLOT_SYNC_SPIN (1u << 22)   // 0 in the test build lib/libqtesla_ntt_syncfail.so: every wait expires
 #endif
@@ -145,7 +136,6 @@ struct SlotSync {
     template <int G>
     __device__ __forceinline__ void wait()
     {
-#if LARGE_SLOT_SYNC
         target += G;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -164,9 +154,6 @@ struct SlotSync {
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
-        __syncthreads();
-#endif
     }
     // after the step's last exchange read: store sentinels from here on?
     __device__ __forceinline__ bool poisoned() const
@@ -175,58 +162,9 @@ struct SlotSync {
     }
 };
 
-// One radix-2 CT stage across waves: this wave and its partner hold the two
-// halves at the same register/lane slots; `hi` = this wave holds the upper
-// (y) half.  lo sends a = x mod 2q (x itself when !RED: inputs < 2q), hi
-// sends tn = -(w y mod q); lo keeps a + t, hi keeps a - t + 2q, in [0,4q).
-// Exchange through the waves' own transpose buffers, layout [j][lane]
-// (conflict-free b32 accesses); the second barrier frees the buffers.
-template <class P, bool RED, int G>
-__device__ __forceinline__ void cross_ct(uint32_t (&r)[32], uint32_t *mine, const uint32_t *theirs, uint32_t lane, bool hi,
-                                         uint2 w, SlotSync &ss)
-{
-    if (hi) {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) r[j] = madlo32(__umulhi(r[j], w.y), P::Q, r[j] * w.x);
-    } else if (RED) {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) r[j] = csub<P::Q2>(r[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 32; ++j) mine[j * 64 + lane] = r[j];
-    ss.wait<G>();
-    if (hi) {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) r[j] = theirs[j * 64 + lane] + r[j] + 2 * P::Q;
-    } else {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) r[j] = r[j] - theirs[j * 64 + lane];
-    }
-    ss.wait<G>();
-}
-
-// One GS stage across waves, inputs and outputs in [0,2q): lo keeps
-// (x + y) mod 2q, hi keeps (x - y) w by the signed Shoup product.
-template <class P, int G>
-__device__ __forceinline__ void cross_gs(uint32_t (&r)[32], uint32_t *mine, const uint32_t *theirs, uint32_t lane, bool hi,
-                                         uint2 w, SlotSync &ss)
-{
-#pragma unroll
-    for (int j = 0; j < 32; ++j) mine[j * 64 + lane] = r[j];
-    ss.wait<G>();
-    if (hi) {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) r[j] = sshoup_mul<P::Q>(theirs[j * 64 + lane] - r[j], w.x, w.y);
-    } else {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) r[j] = csub<P::Q2>(r[j] + theirs[j * 64 + lane]);
-    }
-    ss.wait<G>();
-}
-
-// ---- in-register head (LARGE_HEAD) -----------------------------------------
-// The standalone transforms can run the g = log2 G stages on pos bits L-1 ..
-// 11 in registers instead of across waves: wave B loads chunk c's words
+// ---- in-register head -------------------------------------------------------
+// The g = log2 G stages on pos bits L-1 .. 11 run in registers instead of
+// across waves: wave B loads chunk c's words
 // 2048 c + (2048/G) B + p (p < 2048/G) at register (32/G) c + j'
 // (p = 64 j' + l: G runs of 8/G KiB), so every radix-G group of a lane is
 // registers j', 32/G + j', ...; the head's butterflies and twiddles are the
@@ -234,13 +172,8 @@ __device__ __forceinline__ void cross_gs(uint32_t (&r)[32], uint32_t *mine, cons
 // (register (32/G) B' + j' = sub-block word (2048/G) B' + 64 j' + l, the
 // pass-1 layout): only the other waves' chunks move, (G-1)/G of the 32
 // words, one LDS round trip and two slot barriers in place of the cross
-// stages' g round trips of all 32 words and 2g barriers.
-#ifndef LARGE_HEAD
-#define LARGE_HEAD 1
-#endif
-#ifndef LARGE_HEAD_SKIPOWN
-#define LARGE_HEAD_SKIPOWN 1   // own chunk stays in registers (else it round-trips too)
-#endif
+// stages' g round trips of all 32 words and 2g barriers (session 2 of round 3:
+// n = 8192 products -8.5 / -6.7 %, profiles/r03/ab_large_head_products.log).
 template <class P, int G>
 __device__ __forceinline__ void head_fwd(uint32_t (&r)[32], const uint2 *cross)
 {
@@ -279,7 +212,8 @@ __device__ __forceinline__ void head_inv(uint32_t (&r)[32], const uint2 *cross)
     for (int j = 0; j < H; ++j) gs_bfly<P::Q>(r[j], r[H + j], w1.x, w1.y);
 }
 // chunk c of wave B <-> chunk B of wave c among the slot's G waves (buffers
-// [j][lane], conflict-free; chunk B stays in registers); the second wait frees
+// [j][lane], conflict-free; chunk B stays in registers, it does not
+// round-trip through LDS); the second wait frees
 // the buffers for the next transpose / exchange
 template <int G>
 __device__ __forceinline__ void head_exchange(uint32_t (&r)[32], uint32_t *mine, const uint32_t *slot_bufs, uint32_t lane,
@@ -288,13 +222,13 @@ __device__ __forceinline__ void head_exchange(uint32_t (&r)[32], uint32_t *mine,
     constexpr int C = 32 / G;
 #pragma unroll
     for (int c = 0; c < G; ++c)
-        if (!LARGE_HEAD_SKIPOWN || (uint32_t)c != B)
+        if ((uint32_t)c != B)
 #pragma unroll
             for (int j = 0; j < C; ++j) mine[(C * c + j) * 64 + lane] = r[C * c + j];
     ss.wait<G>();
 #pragma unroll
     for (int c = 0; c < G; ++c)
-        if (!LARGE_HEAD_SKIPOWN || (uint32_t)c != B) {
+        if ((uint32_t)c != B) {
             const uint32_t *src = slot_bufs + c * XPOSE_WORDS + B * C * 64 + lane;
 #pragma unroll
             for (int j = 0; j < C; ++j) r[C * c + j] = src[j * 64];
@@ -313,8 +247,9 @@ __device__ __forceinline__ uint32_t xch_pos(uint32_t kp, uint32_t B)
     return (kp + B * (32u / G)) & 2047u;
 }
 
-// The workgroup's twiddle tables of one direction into LDS at `tab`: T_0's
-// lane image, then the bit-5 table of every B (SHARED), else the G images.
+// The workgroup's twiddle tables of one direction into LDS at `tab`: per B
+// the compact image (INC), else T_0's lane image (the bit-5 pairs come from
+// __constant__ memory).
 template <class LG, bool INV>
 __device__ __forceinline__ void fill_large_tw(uint32_t *tab)
 {
@@ -327,16 +262,7 @@ __device__ __forceinline__ void fill_large_tw(uint32_t *tab)
         }
         return;
     }
-    if constexpr (!LG::SHARED) {   // the G images, contiguous in g_tw2imgL
-        const uint4 *src = g_tw2imgL[LG::IDX][INV ? 1 : 0][0];
-        for (int i = threadIdx.x; i < LG::G * TW2_VEC4; i += LG::NT) dst[i] = src[i];
-        return;
-    }
-    for (int i = threadIdx.x; i < TW2_BIT5_VEC4 + (LG::BIT5U ? 0 : LG::G * 16); i += LG::NT) {
-        const int b = i < TW2_BIT5_VEC4 ? 0 : (i - TW2_BIT5_VEC4) >> 4;
-        const int o = i < TW2_BIT5_VEC4 ? i : TW2_BIT5_VEC4 + ((i - TW2_BIT5_VEC4) & 15);
-        dst[i] = g_tw2imgL[LG::IDX][INV ? 1 : 0][b][o];
-    }
+    for (int i = threadIdx.x; i < TW2_BIT5_VEC4; i += LG::NT) dst[i] = g_tw2imgL[LG::IDX][INV ? 1 : 0][0][i];
 }
 
 // register j of the pass-2 layout times F_B[j] / G_B[j] (Shoup, output in [0, 2q))
@@ -355,7 +281,7 @@ __device__ __forceinline__ void subtree_scale(uint32_t (&r)[32], uint32_t B)
 
 // Per-wave state of the large-n kernels: the wave's sub-block B and slot,
 // its exchange buffer, the slot barrier and, per direction, the lane table
-// (T_0's when SHARED, else T_B's image) and T_B's bit-5 table.
+// (T_0's when SHARED, else T_B's compact image) and T_B's bit-5 table.
 template <class LG>
 struct LargeWave {
     using P = typename LG::P;
@@ -394,12 +320,9 @@ struct LargeWave {
         if constexpr (LG::INC) {
             tw2[D] = reinterpret_cast<const uint2 *>(t + B * LG::CTAB_WORDS);
             bit5[D] = tw2[D] + LG::INC_ENTRIES * 64;
-        } else if constexpr (LG::BIT5U) {
+        } else {
             tw2[D] = reinterpret_cast<const uint2 *>(t);
             bit5[D] = c_bit5L[LG::IDX][D][B];
-        } else {
-            tw2[D] = reinterpret_cast<const uint2 *>(t + (LG::SHARED ? 0u : B * TW2_WORDS));
-            bit5[D] = LG::SHARED ? reinterpret_cast<const uint2 *>(t + TW2_BIT5_VEC4 * 4 + B * 64) : tw2[D] + TW2_ENTRIES * 64;
         }
     }
     // Re-derive the wave-uniform state from an opaque wave index at the top of
@@ -422,57 +345,29 @@ struct LargeWave {
         ss.ctr = ctrs + slot;
         ss.poison = ctrs + LG::SLOTS;
     }
-    __device__ __forceinline__ const uint32_t *partner(uint32_t d) const { return lds + (wave ^ d) * XPOSE_WORDS; }
-
-    // forward of this wave's share (sub-block B words 2048 B + p', inputs
-    // < 2q at register j of lane l = p' 64 j + brl) down to the pass-2
-    // layout: register j of lane l holds sub-block output k' = brv5(j) 64 + l
-    // of global index G k' + brv_g(B), in [0,4q)
-    // (LARGE_HEAD: the input is in the head's chunked layout instead, see
-    // head_fwd, and the first g stages run in registers + one exchange)
+    // forward of this wave's share (the head's chunked layout, see head_fwd,
+    // inputs < 2q; the first g stages run in registers + one exchange) down
+    // to the pass-2 layout: register j of lane l holds sub-block output
+    // k' = brv5(j) 64 + l of global index G k' + brv_g(B), in [0,4q)
     template <int BMIN = 0>
     __device__ __forceinline__ void fwd(uint32_t (&r)[32])
     {
         constexpr int G = LG::G;
-        if constexpr (LARGE_HEAD) {
-            head_fwd<P, G>(r, c_cross[LG::IDX][0]);
-            head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, opaque_lane(), B, ss);
-        } else {
-            constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1), then for n = 8192 pos bit 11 (k = 2 + B/2)
-            cross_ct<P, false, G>(r, buf, partner(D0), opaque_lane(), (B & D0) != 0, c_cross[LG::IDX][0][1], ss);
-            if constexpr (G == 4)
-                cross_ct<P, true, G>(r, buf, partner(1u), opaque_lane(), (B & 1u) != 0, c_cross[LG::IDX][0][2 + (B >> 1)], ss);
-        }
+        head_fwd<P, G>(r, c_cross[LG::IDX][0]);
+        head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, opaque_lane(), B, ss);
         fwd_pass1_tw<P, true, LG::BIT5U>(r, L.h, c_subtw[LG::IDX][0][B] + opaque_zero(), bit5[0] + opaque_zero());
         lds_p1_to_p2<P>(r, buf, LT(opaque_lane()));   // addresses recomputed (see inv)
         subtree_scale<P, LG, false>(r, B);             // T_B = c_{B,b} T_0 (c_fscale)
         fwd_pass2<P, BMIN>(r, tw2[0] + opaque_zero(), L.lane);
     }
-    // all-to-all through the exchange buffers: from the pass-2 layout to
-    // global words [2048 B, 2048 B + 2048) at register j of lane l = word
-    // 64 j + l (lane-contiguous runs), canonical
-    __device__ __forceinline__ void to_contiguous(uint32_t (&r)[32])
-    {
-        constexpr int G = LG::G;
-        const uint32_t lane = opaque_lane();   // addresses recomputed per step, not hoisted into VGPRs
-#pragma unroll
-        for (int j = 0; j < 32; ++j) buf[xch_pos<G>(brv5(j) * 64 + lane, B)] = canon4<P>(r[j]);
-        ss.template wait<G>();
-        {
-            const uint32_t bs = brv_g(lane % G, LG::LOGG);   // source wave of global word g (g = lane mod G)
-            const uint32_t *src = lds + (slot * G + bs) * XPOSE_WORDS;
-            const uint32_t k0 = 2048u / G * B + lane / G;     // k' of j = 0
-#pragma unroll
-            for (int j = 0; j < 32; ++j) r[j] = src[xch_pos<G>(k0 + 64u / G * j, bs)];
-        }
-        ss.template wait<G>();   // the buffers are free for the next exchanges
-    }
-    // the inverse of to_contiguous (no reduction): contiguous words scattered
-    // to the owning waves, back in the pass-2 layout (the buffers must be free)
+    // contiguous words (global words [2048 B, 2048 B + 2048) at register j of
+    // lane l = word 64 j + l) scattered to the owning waves, into the pass-2
+    // layout (the buffers must be free).  Position of sub-block output k' in
+    // its wave's buffer: xch_pos (conflict-free both ways)
     __device__ __forceinline__ void from_contiguous(uint32_t (&r)[32])
     {
         constexpr int G = LG::G;
-        const uint32_t lane = opaque_lane();   // (see to_contiguous)
+        const uint32_t lane = opaque_lane();   // addresses recomputed per step, not hoisted into VGPRs
         {
             const uint32_t bt = brv_g(lane % G, LG::LOGG);   // owner of g (g = lane mod G)
             uint32_t *dst = lds + (slot * G + bt) * XPOSE_WORDS;
@@ -485,7 +380,7 @@ struct LargeWave {
         for (int j = 0; j < 32; ++j) r[j] = buf[xch_pos<G>(brv5(j) * 64 + lane, B)];
     }
     // inverse from the pass-2 layout (inputs < 2q) to this wave's share of
-    // the natural order (word 2048 B + 64 j + brl at register j), [0,2q),
+    // the natural order in the head's chunked layout (large_off), [0,2q),
     // scaled by n^-1 (RS: and by 2^32, undoing a Montgomery product's 2^-32)
     // RS 0: plain inverse; 1: also times 2^32 (undoes a Montgomery product's
     // 2^-32); 2: the incomplete-domain product's -- from pos bit BMIN (WIDE0:
@@ -504,15 +399,8 @@ struct LargeWave {
         inv_pass1_head<P, LG::BIT5U>(r, L.h, c_subtw[LG::IDX][1][B] + opaque_zero(), bit5[1] + opaque_zero());
         const uint2 last = c_lastinv[LG::IDX][RS][B];
         inv_last_stage<P, false>(r, NINV, NINVP, last.x, last.y);   // [0,2q)
-        if constexpr (LARGE_HEAD) {   // output in the head's chunked layout
-            head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, opaque_lane(), B, ss);
-            head_inv<P, G>(r, c_cross[LG::IDX][1]);
-        } else {
-            if constexpr (G == 4)   // pos bit 11 (k = 2 + B/2)
-                cross_gs<P, G>(r, buf, partner(1u), opaque_lane(), (B & 1u) != 0, c_cross[LG::IDX][1][2 + (B >> 1)], ss);
-            constexpr uint32_t D0 = G / 2;   // pos bit L-1 (k = 1)
-            cross_gs<P, G>(r, buf, partner(D0), opaque_lane(), (B & D0) != 0, c_cross[LG::IDX][1][1], ss);
-        }
+        head_exchange<G>(r, buf, lds + slot * G * XPOSE_WORDS, opaque_lane(), B, ss);   // the head's chunked layout
+        head_inv<P, G>(r, c_cross[LG::IDX][1]);
     }
 };
 
@@ -536,18 +424,17 @@ __device__ __forceinline__ void large_steps(const LargeWave<LG> &w, uint32_t fir
     }
 }
 
-// Word offset of register j from a wave's first word: the contiguous
-// sub-block layout (64 j), or with LARGE_HEAD the head's chunks (chunk c =
-// j / (32/G) at 2048 c); the wave's first word is 2048 B resp. (2048/G) B.
+// Word offset of register j from a wave's first word in the head's chunks
+// (chunk c = j / (32/G) at 2048 c); the wave's first word is (2048/G) B.
 template <class LG>
 __host__ __device__ constexpr uint32_t large_off(int j)
 {
-    return LARGE_HEAD ? 2048u * (uint32_t)(j / (32 / LG::G)) + 64u * (uint32_t)(j % (32 / LG::G)) : 64u * (uint32_t)j;
+    return 2048u * (uint32_t)(j / (32 / LG::G)) + 64u * (uint32_t)(j % (32 / LG::G));
 }
 template <class LG>
 __device__ __forceinline__ uint32_t large_first(uint32_t B)
 {
-    return LARGE_HEAD ? B * (2048u / LG::G) : B * 2048u;
+    return B * (2048u / LG::G);
 }
 
 // the step's stores: a poisoned workgroup (expired slot barrier) writes sentinels
@@ -559,9 +446,6 @@ __device__ __forceinline__ void large_store(uint32_t *dst, const LargeWave<LG> &
     for (int j = 0; j < 32; ++j) st_out(dst + large_off<LG>(j), bad ? SYNC_SENTINEL : val(j));
 }
 
-#ifndef MUL_PF
-#define MUL_PF 1
-#endif
 // Fused product c = a*b mod (x^n + 1) for n = 4096 / 8192: FWD(a) and FWD(b)
 // (or b-hat = poly_ntt(b), natural order, brought to the pass-2 layout by the
 // contiguous-load scatter: BHAT) meet in the pass-2 layout, where the
@@ -570,51 +454,35 @@ __device__ __forceinline__ void large_store(uint32_t *dst, const LargeWave<LG> &
 // inverse's scatter of a separate pipeline never happen, one HBM read of a
 // and b, one write of c.  a, b and c may alias: the G waves of a slot load
 // all of a and b before the slot barriers that precede any store.
-#ifndef MUL_LARGE_WAVES
-#define MUL_LARGE_WAVES 12   // n = 8192 product with both operands transformed: with the cross-wave
-                              // stages 8 waves at 2 per SIMD (199 VGPRs) beat 12 at 3 (37 VGPRs
-                              // spilled), 6.68 vs 6.77 ms (profiles/r03/ab_mul_large.log); with the
-                              // in-register head 12 waves spill 5: 6.09 -> 5.93 ms per 2^17 products
-                              // (profiles/r03/ab_mul_large_w12.log)
-#endif
-#ifndef MUL_LARGE_INC
-#define MUL_LARGE_INC 1   // poly_mul (not poly_mul_ntt) in the incomplete domain
-#endif
+// poly_mul (not poly_mul_ntt) in the incomplete domain (5.88 -> 4.72 ms per
+// 2^17 products, profiles/r04/k)
 template <int PS, bool BHAT>
 constexpr bool mul_large_inc()
 {
-    return !BHAT && MUL_LARGE_INC;
+    return !BHAT;
 }
 #ifndef MUL_LARGE_INC_WAVES
 #define MUL_LARGE_INC_WAVES 8   // two 8-wave workgroups per CU (78 KiB LDS each): no full-CU drain between workgroups
 #endif
-#ifndef MUL_LARGE_BIT5U
-#define MUL_LARGE_BIT5U 1   // poly_mul_ntt: bit-5 pairs from __constant__, 16 waves
-#endif
-template <int PS, bool BHAT>
-constexpr bool mul_large_bit5u()
-{
-    return BHAT && MUL_LARGE_BIT5U;
-}
 template <int PS, bool BHAT>
 constexpr int mul_large_waves()
 {
     // the incomplete domain's compact tables leave room for two 8-wave
     // workgroups per CU (4 waves per SIMD, 4.92 -> 4.55 ms per 2^20 products,
     // profiles/r04/s); the shared table without its bit-5 pairs for 16 waves
-    return mul_large_inc<PS, BHAT>() ? MUL_LARGE_INC_WAVES : mul_large_bit5u<PS, BHAT>() ? 16
-           : (PSel<PS>::T::N == 8192 && !BHAT)                         ? MUL_LARGE_WAVES
-                                                                       : 12;
+    return mul_large_inc<PS, BHAT>() ? MUL_LARGE_INC_WAVES : 16;
 }
 template <int PS, bool BHAT>
-using LargeMul = Large<PS, mul_large_waves<PS, BHAT>(), mul_large_inc<PS, BHAT>(), mul_large_bit5u<PS, BHAT>()>;
+using LargeMul = Large<PS, mul_large_waves<PS, BHAT>(), mul_large_inc<PS, BHAT>()>;
 template <int PS, bool BHAT>
 __global__ __launch_bounds__((LargeMul<PS, BHAT>::NT), (LargeMul<PS, BHAT>::OCC))
 void k_poly_mul_large(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t ppw)
 {
     using LG = LargeMul<PS, BHAT>;
     using P = typename LG::P;
-    constexpr bool PF = MUL_PF && !(LG::G == 4 && !BHAT);
+    // both operands' loads up front, except for the n = 8192 poly_mul (its
+    // b loads follow a's forward: register pressure)
+    constexpr bool PF = !(LG::G == 4 && !BHAT);
     __shared__ __attribute__((aligned(16))) uint32_t lds[LG::LDS_WORDS];
     const uint32_t first = blockIdx.x * (LG::SLOTS * ppw);
     if (first >= npoly) return;

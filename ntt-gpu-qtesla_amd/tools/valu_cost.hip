@@ -70,6 +70,42 @@ K32(v_add_co_u32, "v_add_co_u32 %0, vcc, %0, %1")
 K32(v_addc_co_u32, "v_addc_co_u32 %0, vcc, %0, %1, vcc")
 K32(v_cmp_lt_u32, "v_cmp_lt_u32 vcc, %0, %1")
 K32(v_bfe_u32, "v_bfe_u32 %0, %0, 1, 7")
+// round 5: every other opcode the product kernels emit (tools/asm_hist.py over
+// `make asm`), so the VALU roofline's mean cost has no guessed term
+K32(v_sub_co_u32, "v_sub_co_u32 %0, vcc, %0, %1")
+K32(v_subrev_co_u32, "v_subrev_co_u32 %0, vcc, %0, %1")
+K32(v_subb_co_u32, "v_subb_co_u32 %0, vcc, %0, %1, vcc")
+K32(v_subbrev_co_u32, "v_subbrev_co_u32 %0, vcc, %0, %1, vcc")
+K32(v_cmp_gt_u32, "v_cmp_gt_u32 vcc, %0, %1")
+K32(v_cmp_ne_u32, "v_cmp_ne_u32 vcc, %0, %1")
+K32(v_cmp_eq_u32, "v_cmp_eq_u32 vcc, %0, %1")
+K32(v_cmp_le_u32, "v_cmp_le_u32 vcc, %0, %1")
+K32(v_cmp_gt_u16, "v_cmp_gt_u16 vcc, %0, %1")
+K32(v_not_b32, "v_not_b32 %0, %0")
+K32(v_alignbit_b32, "v_alignbit_b32 %0, %0, %0, 1")
+K32(v_bfrev_b32, "v_bfrev_b32 %0, %0")
+K32(v_xad_u32, "v_xad_u32 %0, %0, %1, %1")
+K32(v_or3_b32, "v_or3_b32 %0, %0, %1, %1")
+K32(v_mad_u32_u24, "v_mad_u32_u24 %0, %0, %1, %1")
+K32(v_mul_lo_u16, "v_mul_lo_u16 %0, %0, %1")
+K32(v_sub_u16, "v_sub_u16 %0, %0, %1")
+K32(v_mbcnt_lo_u32_b32, "v_mbcnt_lo_u32_b32 %0, %1, %0")
+K32(v_mbcnt_hi_u32_b32, "v_mbcnt_hi_u32_b32 %0, %1, %0")
+// v_readfirstlane_b32: VALU op with an SGPR destination, 8 independent ones
+__global__ __launch_bounds__(256) void k_v_readfirstlane_b32(unsigned *out, unsigned seed, int iters)
+{
+    unsigned a[8], m[8];
+    for (int k = 0; k < 8; k++) a[k] = (threadIdx.x ^ seed) + k;
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(m[k]) : "v"(a[k]));
+    }
+    unsigned r = 0;
+    for (int k = 0; k < 8; k++) r ^= a[k] ^ m[k];
+    out[blockIdx.x * 256 + threadIdx.x] = r;
+}
 // v_cndmask with its condition in an SGPR pair that nothing in the loop
 // writes (the K32 form above clobbers vcc in every asm statement)
 #define KSEL(NAME, ASM)                                                                   \
@@ -97,6 +133,10 @@ K64(v_mad_i64_i32, "v_mad_i64_i32 %0, vcc, %1, %1, %0")
 K64(v_lshl_add_u64, "v_lshl_add_u64 %0, %0, 1, %0")
 K64(v_lshlrev_b64, "v_lshlrev_b64 %0, 1, %0")
 K64(v_mov_b64, "v_mov_b64 %0, %0")
+K64(v_lshrrev_b64, "v_lshrrev_b64 %0, 1, %0")
+K64(v_pk_mov_b32, "v_pk_mov_b32 %0, %0, %0 op_sel:[1,0]")
+K64(v_cmp_gt_u64, "v_cmp_gt_u64 vcc, %0, %0")
+K64(v_cmp_le_u64, "v_cmp_le_u64 vcc, %0, %0")
 
 __global__ __launch_bounds__(256) void k_v_permlane32_swap_b32(unsigned *out, unsigned seed, int iters)
 {
@@ -135,6 +175,11 @@ int main(int argc, char **argv)
               E(v_and_or_b32), E(v_mul_lo_u32), E(v_mul_hi_u32), E(v_mul_hi_i32), E(v_mul_u32_u24),
               E(v_cndmask_b32), E(v_cndmask_b32_sgpr), E(v_cndmask_b32_sgpr_neg), E(v_add_co_u32), E(v_addc_co_u32), E(v_cmp_lt_u32), E(v_bfe_u32),
               E(v_mad_u64_u32), E(v_mad_i64_i32), E(v_lshl_add_u64), E(v_lshlrev_b64), E(v_mov_b64),
+              E(v_sub_co_u32), E(v_subrev_co_u32), E(v_subb_co_u32), E(v_subbrev_co_u32), E(v_cmp_gt_u32),
+              E(v_cmp_ne_u32), E(v_cmp_eq_u32), E(v_cmp_le_u32), E(v_cmp_gt_u16), E(v_not_b32), E(v_alignbit_b32),
+              E(v_bfrev_b32), E(v_xad_u32), E(v_or3_b32), E(v_mad_u32_u24), E(v_mul_lo_u16), E(v_sub_u16),
+              E(v_mbcnt_lo_u32_b32), E(v_mbcnt_hi_u32_b32), E(v_readfirstlane_b32), E(v_lshrrev_b64), E(v_pk_mov_b32),
+              E(v_cmp_gt_u64), E(v_cmp_le_u64),
               {"v_permlane32_swap_b32", k_v_permlane32_swap_b32, 16}};
     hipEvent_t e0, e1;
     hipEventCreate(&e0);

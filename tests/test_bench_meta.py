@@ -76,15 +76,44 @@ def test_load_pmc_reports_stale_build(ntt):
 def test_valu_roofline_fields():
     """VALU-bound ops report roofline.bound "valu": SIMD issue cycles per
     launch (SQ_INSTS_VALU x mean opcode cost) over the live launch time,
-    against 4 SIMDs x CUs x 2.4 GHz, with the HBM fraction kept beside it."""
+    against 4 SIMDs x CUs x 2.4 GHz, with the HBM fraction kept beside it.
+    The held-clock fraction comes from the counter pass alone (its busy value),
+    whatever this run's launch time is."""
     v = {"valu_simd_cycles_per_launch": 1024 * 2.4e9 * 5e-3, "clock_ghz_pmc": 2.0, "cus": 256,
-         "SQ_INSTS_VALU": 1.0, "mean_simd_cycles_per_valu": 3.5}
+         "SQ_INSTS_VALU": 1.0, "mean_simd_cycles_per_valu": 3.5, "valu_busy_at_pmc_clock": 0.87,
+         "uncosted_opcodes": {}}
     r = bench.valu_roofline(v, 10.0, {"bound": "hbm", "frac": 0.4})
     assert r["bound"] == "valu" and r["unit"] == "G SIMD-cycles/s"
-    assert abs(r["frac"] - 0.5) < 1e-12 and abs(r["frac_at_held_clock"] - 0.6) < 1e-12
+    assert abs(r["frac"] - 0.5) < 1e-12 and r["frac_at_held_clock"] == 0.87
+    assert bench.valu_roofline(v, 7.0, {})["frac_at_held_clock"] == 0.87   # independent of the live time
     assert r["hbm"]["frac"] == 0.4
     assert bench.valu_roofline(None, 10.0, {})["frac"] is None
     assert {"polymul", "polymul_ntt", "nussbaumer"} == bench.VALU_BOUND
+
+
+def _valu_entries():
+    with open(bench.PMC_PATH) as f:
+        entries = json.load(f)["entries"]
+    return {w: e for w, e in entries.items() if "valu" in e}
+
+
+def test_valu_entries_fully_costed():
+    """Every VALU opcode the measured kernels emit has a measured issue cost
+    (tools/valu_cost.hip), so the mean cycles per instruction carries no
+    guessed term; the held-clock fraction the line reports is the entry's own
+    busy value (one counter pass: VALU SIMD-cycles over its GRBM cycles)."""
+    ents = _valu_entries()
+    assert ents
+    tree = _tree_hash()
+    if tree is not None and any(e.get("build_hash") != tree for e in ents.values()):
+        pytest.xfail("profiles/pmc_summary.json VALU entries were measured on another build")
+    for w, e in ents.items():
+        for key, k in e["valu"]["kernels"].items():
+            assert k["uncosted_opcodes"] == {}, (w, key, k["uncosted_opcodes"])
+            busy = k["valu_simd_cycles_per_launch"] / (4 * e["valu"].get("cus", 256) * k["GRBM_GUI_ACTIVE_per_xcd"])
+            assert abs(busy - k["valu_busy_at_pmc_clock"]) < 0.01 * busy, (w, key)
+            r = bench.valu_roofline(dict(k, cus=e["valu"].get("cus", 256)), 1.0, {})
+            assert abs(r["frac_at_held_clock"] - k["valu_busy_at_pmc_clock"]) < 0.01 * k["valu_busy_at_pmc_clock"]
 
 
 def test_valu_cost_table_classes():

@@ -102,7 +102,7 @@ def test_typed_ct_butterfly(name, xs, ys, yos):
 @pytest.mark.parametrize("name", list(PRIMES))
 def test_canonical_stage0_and_s_canon(name):
     """stage 0 of fwd_pass1_lz: canonical inputs, no reduction, S output; and
-    BaseMul::canon / the NTT_FWD_LZ store: (-2q, 2q) -> [0, q) by
+    BaseMul::canon: (-2q, 2q) -> [0, q) by
     min(x, x + 2q) then one conditional subtraction of q"""
     q = PRIMES[name]
     rng = random.Random(7)
@@ -204,7 +204,8 @@ def test_zeta_split_residue_product(name):
 
 @pytest.mark.parametrize("name", list(PRIMES))
 def test_half_canonical_residue_product_and_wide_first_stage(name):
-    """MUL_AHALF (p-III, where the z-split output needs its csub anyway):
+    """BaseMul::AH, the half-canonical a (p-III, where the z-split output
+    needs its csub anyway):
     a in [0, 2q), b canonical -> c_k < 16 q^2 fits 64 bits with the REDC's
     m q; the REDC output after one csub lies below 2.19 q (p-III), and the
     inverse's first GS stage (inv_pass2 WIDE0) maps such x, y to

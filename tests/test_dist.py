@@ -59,6 +59,9 @@ def test_bench_launcher_free_ranks_fail_loudly_without_devices():
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    # no device visible to the children, whatever the machine has (on an
+    # 8-GPU box this CPU test must not start a real 2-rank bench)
+    env.update(HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--batch", "64",
                         "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=root)

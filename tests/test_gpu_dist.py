@@ -112,3 +112,26 @@ def test_bench_refuses_more_ranks_than_devices(ntt):
     assert r.returncode != 0
     assert "visible device" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.parametrize("config", [4, 5])
+def test_bench_two_ranks_product_configs(ntt, config):
+    """BASELINE's multi-GPU config is the poly-mul (config 4, 2^23 sharded
+    over 8 GPUs); config 5 (Nussbaumer) shards the same way.  Rehearsed here
+    through bench.py's own launcher-free spawn, its checker legs and its
+    global_batch accounting, with the VALU roofline block of a product line."""
+    batch, steps = 4096, 2
+    r = _bench(["--config", str(config), "--gpus", "2", "--allow-shared-devices", "--batch", str(batch),
+                "--steps", str(steps), "--warmup", "1", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * batch
+    assert d["check"]["all_ranks_ok"] is True
+    assert d["check"]["sampled_vs_oracle"]["ok"] is True
+    assert d["unit"] == "products/s"
+    roof = d["roofline"]
+    assert roof["bound"] == "valu" and roof["unit"] == "G SIMD-cycles/s" and roof["hbm"]["bound"] == "hbm"
+    assert roof["kernel"] == ("mul" if config == 4 else "nus")
+    assert abs(d["value"] - 2 * batch * steps / (d["ms_per_step"] * steps * 1e-3)) <= 1e-6 * d["value"]
