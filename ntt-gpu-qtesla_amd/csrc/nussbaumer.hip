@@ -69,10 +69,18 @@ constexpr int NUS_WAVES = NUS_WG / 64;
 constexpr int NUS_PAIRS = NUS_WAVES / 2;
 constexpr int NUS_MAT_WORDS = 4096;             // one 64-row x R x H matrix (16 KiB)
 constexpr int NUS_PAIR_WORDS = 2 * NUS_MAT_WORDS;
-#ifndef NUS_PPW_CFG
-#define NUS_PPW_CFG 1   // one unit per workgroup (no table prologue to amortise): 2 % faster than 16, profiles/r02/s4/ab_nussbaumer_ppw.log
+// units per workgroup, per ring.  Z/q: one (no table prologue to amortise;
+// 2 % faster than 16 without the prefetch, profiles/r02/s4/ab_nussbaumer_ppw.log,
+// and the prefetch does not pay there: p-III 17.68 -> 17.82 ms at 16,
+// profiles/r05/b).  Z/(2^32-1): 16 with the next unit's loads prefetched,
+// 21.89 -> 21.47 ms (p-III's n = 2048, profiles/r05/b)
+#ifndef NUS_PPW_Q
+#define NUS_PPW_Q 1
 #endif
-constexpr int NUS_PPW_MAX = NUS_PPW_CFG;
+#ifndef NUS_PPW_M32
+#define NUS_PPW_M32 16
+#endif
+template <int RING> constexpr int nus_ppw_max() { return RING == NTT_RING_M32 ? NUS_PPW_M32 : NUS_PPW_Q; }
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F &&f)
@@ -91,6 +99,27 @@ __host__ __device__ constexpr int cbrv(int x, int bits)
 }
 
 __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+// Phase stamps, diagnostic builds only (-DNUS_STAMPS, tools/nus_stamps.py):
+// s_memtime at the phase boundaries of a unit, after `dep` is computed,
+// written by lane 0 of each wave of the first NUS_STAMP_WGS workgroups with
+// a vector store (the last unit of a workgroup wins).  In the product build
+// NUS_STAMP expands to nothing.
+#ifdef NUS_STAMPS
+constexpr int NUS_STAMP_N = 16;
+constexpr int NUS_STAMP_WGS = 8192;
+__device__ unsigned long long g_nus_stamps[NUS_STAMP_WGS * 2][NUS_STAMP_N];
+__device__ __forceinline__ void nus_stamp(int k, uint32_t dep)
+{
+    asm volatile("" ::"v"(dep));
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (blockIdx.x < (uint32_t)NUS_STAMP_WGS && (threadIdx.x & 63) == 0)
+        g_nus_stamps[blockIdx.x * 2 + ((threadIdx.x >> 6) & 1)][k] = t;
+}
+#define NUS_STAMP(k, dep) nus_stamp(k, dep)
+#else
+#define NUS_STAMP(k, dep) ((void)0)
+#endif
 
 // LDS hand-offs between the two waves of a pair: a workgroup barrier (the
 // workgroup is one pair; with several pairs per workgroup every pair runs the
@@ -500,10 +529,51 @@ __device__ __forceinline__ uint32_t mat_off(uint32_t h, int k, uint32_t a)
     return (h * 64 + k) * R + (a ^ (swz<R>(k) << 2));
 }
 
+// The 32 input words of a lane for unit u (raw, before in_x / in_b): lane
+// a of half h holds words 32 a .. 32 a + 31 of product u H + h.  Loads are
+// unconditional: an idle half-wave (odd n=1024 batch) reads the unit's
+// first product and never stores; both waves of the pair load the same
+// words (the implicit first stage copies sub-polynomial k to k + 32).
+template <int PS>
+__device__ __forceinline__ void nus_load(const uint32_t *a, const uint32_t *b, uint32_t npoly, uint32_t u,
+                                         uint32_t (&X)[32], uint32_t (&Y)[32])
+{
+    using P = typename PSel<PS>::T;
+    using G = Geo<P::N>;
+    uint32_t lane = threadIdx.x & 63u;
+    asm volatile("" : "+v"(lane));
+    const uint32_t ca = lane & (G::R - 1), h = lane / G::R;
+    const uint32_t poly = u * G::H + h;
+    const size_t loff = (size_t)(poly < npoly ? poly : u * G::H) * P::N + 32u * ca;
+#pragma unroll
+    for (int q4 = 0; q4 < 8; ++q4) {
+        const uint4 x = *(const uint4 *)(a + loff + 4 * q4);
+        const uint4 y = *(const uint4 *)(b + loff + 4 * q4);
+        X[4 * q4 + 0] = x.x;
+        X[4 * q4 + 1] = x.y;
+        X[4 * q4 + 2] = x.z;
+        X[4 * q4 + 3] = x.w;
+        Y[4 * q4 + 0] = y.x;
+        Y[4 * q4 + 1] = y.y;
+        Y[4 * q4 + 2] = y.z;
+        Y[4 * q4 + 3] = y.w;
+    }
+}
+
 // One unit (one n=2048 product or two n=1024 products) by wave W of a pair.
-template <int PS, int RING, int W>
+// X / Y: this unit's raw input words (nus_load).  The next unit (u_next,
+// npoly_next) is loaded into X / Y while this one runs -- issued once the
+// inner level's results are in LDS (the register peak is past), so its HBM
+// latency hides behind the recombination, the outer inverse and the stores
+// instead of stalling the next unit's start (PF: the launch runs several units
+// per workgroup).  The load is unconditional (a workgroup's last unit reloads
+// itself, unused): a branch around it would end in a join that waits for the
+// loads on the spot.  `last`: the workgroup's last unit skips the final
+// barrier (it only frees the exchange area for a next unit).
+template <int PS, int RING, int W, bool PF>
 __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t npoly, uint32_t u,
-                                         uint32_t *pl)
+                                         uint32_t *pl, uint32_t (&X)[32], uint32_t (&Y)[32], uint32_t u_next,
+                                         uint32_t npoly_next, bool last)
 {
     using P = typename PSel<PS>::T;
     using G = Geo<P::N>;
@@ -523,26 +593,15 @@ __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, u
     const uint32_t a4 = ca * 4, hb4 = h * R * 4;
     const uint32_t poly = u * H + h;
     const bool valid = poly < npoly;
-    // loads are unconditional: an idle half-wave (odd n=1024 batch) reads the
-    // unit's first product and never stores; both waves of the pair load the
-    // same words (the implicit first stage copies sub-polynomial k to k + 32)
-    const size_t loff = (size_t)(valid ? poly : u * H) * P::N + 32u * ca;
+    NUS_STAMP(0, lane);
 
     {
-        uint32_t X[32], Y[32];
 #pragma unroll
-        for (int q4 = 0; q4 < 8; ++q4) {
-            const uint4 x = *(const uint4 *)(a + loff + 4 * q4);
-            const uint4 y = *(const uint4 *)(b + loff + 4 * q4);
-            X[4 * q4 + 0] = RG::template in_x<G::L>(x.x);
-            X[4 * q4 + 1] = RG::template in_x<G::L>(x.y);
-            X[4 * q4 + 2] = RG::template in_x<G::L>(x.z);
-            X[4 * q4 + 3] = RG::template in_x<G::L>(x.w);
-            Y[4 * q4 + 0] = RG::in_b(y.x);
-            Y[4 * q4 + 1] = RG::in_b(y.y);
-            Y[4 * q4 + 2] = RG::in_b(y.z);
-            Y[4 * q4 + 3] = RG::in_b(y.w);
+        for (int k = 0; k < 32; ++k) {
+            X[k] = RG::template in_x<G::L>(X[k]);
+            Y[k] = RG::in_b(Y[k]);
         }
+        NUS_STAMP(1, X[31] ^ Y[31]);
         outer_fwd_half<RG, G, RG::IN, W>(X, Y, a4, hb4);
         if constexpr (SCH::ROWRED) {
             red_all<RG>(X);
@@ -554,15 +613,19 @@ __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, u
             xm[mat_off<R>(h, 32 * W + k, ca)] = X[k];
             ym[mat_off<R>(h, 32 * W + k, ca)] = Y[k];
         }
+        NUS_STAMP(2, X[31] ^ Y[31]);
     }
     pair_sync();
+    NUS_STAMP(3, lane);
 
     // block W of every row product: lane = sub-polynomial (row), all H products
     uint32_t Zb[H][MI][8];
 #pragma unroll
     for (int hh = 0; hh < H; ++hh)
         inner_block<RG, G, W, SCH::ROW>(Zb[hh], xm + (hh * 64 + lane) * R, ym + (hh * 64 + lane) * R, swz<R>(lane));
+    NUS_STAMP(4, Zb[H - 1][MI - 1][7] ^ Zb[0][0][0]);
     pair_sync();   // both waves are done reading the matrices
+    NUS_STAMP(5, lane);
     uint32_t *const zm = W == 0 ? xm : ym;   // block W's results, same row layout
 #pragma unroll
     for (int hh = 0; hh < H; ++hh) {
@@ -575,7 +638,10 @@ __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, u
                            Zb[hh][(c0 + 2) % MI][(c0 + 2) / MI], Zb[hh][(c0 + 3) % MI][(c0 + 3) / MI]);
         }
     }
+    if constexpr (PF) nus_load<PS>(a, b, npoly_next, u_next, X, Y);   // the next unit's words (see above)
+    NUS_STAMP(6, lane);
     pair_sync();
+    NUS_STAMP(7, lane);
 
     // back in the outer layout for this half: the last inner stage of the two
     // blocks (s, d) and the recombination W[a] = s[a] + d[a - m'], negated
@@ -603,8 +669,10 @@ __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, u
             Z[k] = RG::add(s, RG::negm(d, wmask));
         }
     }
+    NUS_STAMP(8, Z[31] ^ Z[0]);
     outer_inv_half<RG, G, OB::W, W>(Z, a4, hb4);
     constexpr int B5 = stages_out<RG>(OB::W, 5);
+    NUS_STAMP(9, Z[31] ^ Z[0]);
     pair_sync();   // both waves are done reading the block results
 
     // stage 5 (sr = 0) pairs sub-polynomials i and i + 32 across the halves,
@@ -615,7 +683,9 @@ __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, u
 #pragma unroll
         for (int k = 0; k < 16; ++k) xo[k * 64 + lane] = Z[16 * (1 - W) + k];
     }
+    NUS_STAMP(10, lane);
     pair_sync();
+    NUS_STAMP(11, lane);
     const uint32_t *xi = pl + (1 - W) * 1024;
     const uint32_t d1 = a4 - 4, addr1 = (d1 & (4u * R - 1)) | hb4, mask1 = (uint32_t)((int)d1 >> 31);
     constexpr bool FR5 = stage_red<RG>(B5);
@@ -645,7 +715,9 @@ __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, u
         for (int q4 = 0; q4 < 4; ++q4)
             *(uint4 *)(dst + 4 * q4) = make_uint4(o[4 * q4], o[4 * q4 + 1], o[4 * q4 + 2], o[4 * q4 + 3]);
     }
-    pair_sync();   // the exchange area is free for the next unit
+    NUS_STAMP(12, o[15] ^ o[0]);
+    if (!last) pair_sync();   // the exchange area is free for the next unit (wave-uniform, pair-uniform)
+    NUS_STAMP(13, lane);
 }
 
 template <int PS, int RING>
@@ -665,17 +737,32 @@ __global__ __launch_bounds__(NUS_WG, NUS_OCC_CFG) void k_nussbaumer(const uint32
     if (first >= nunits) return;   // whole workgroup idle (uniform)
     const uint32_t wg_units = min((uint32_t)(NUS_PAIRS * ppw), nunits - first);
     const uint32_t steps = (wg_units + NUS_PAIRS - 1) / NUS_PAIRS;
+    // a pair past the batch recomputes the workgroup's first unit and stores nothing
+    auto unit_of = [&](uint32_t v) { return v < nunits ? v : first; };
+    auto np_of = [&](uint32_t v) { return v < nunits ? npoly : 0u; };
+    constexpr bool PF = nus_ppw_max<RING>() > 1;   // several units per workgroup: prefetch the next
+    uint32_t X[32], Y[32];
 #pragma unroll 1
     for (uint32_t it = 0; it < steps; ++it, u += NUS_PAIRS) {
-        // a pair past the batch recomputes the workgroup's first unit and stores nothing
-        const uint32_t uu = u < nunits ? u : first;
-        const uint32_t np = u < nunits ? npoly : 0u;
-        if ((wave & 1) == 0) nus_unit<PS, RING, 0>(a, b, c, np, uu, pl);
-        else nus_unit<PS, RING, 1>(a, b, c, np, uu, pl);
+        if (!PF || it == 0) nus_load<PS>(a, b, np_of(u), unit_of(u), X, Y);
+        const bool last = it + 1 == steps;
+        const uint32_t v = last ? u : u + NUS_PAIRS;   // (the last unit reloads itself, unused)
+        const uint32_t un = unit_of(v), npn = np_of(v);
+        if ((wave & 1) == 0) nus_unit<PS, RING, 0, PF>(a, b, c, np_of(u), unit_of(u), pl, X, Y, un, npn, last);
+        else nus_unit<PS, RING, 1, PF>(a, b, c, np_of(u), unit_of(u), pl, X, Y, un, npn, last);
     }
 }
 
 }  // namespace
+
+#ifdef NUS_STAMPS
+extern "C" int nus_debug_stamps(unsigned long long *host, size_t count)
+{
+    const size_t n = sizeof(g_nus_stamps) / sizeof(unsigned long long);
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_nus_stamps), (count < n ? count : n) * 8, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 
 int nussbaumer_launch(int ps, int ring, const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, void *stream,
                       int cus)
@@ -683,7 +770,8 @@ int nussbaumer_launch(int ps, int ring, const uint32_t *a, const uint32_t *b, ui
     const size_t per_unit = ps == 2 ? 1 : 2;
     const size_t units = (batch + per_unit - 1) / per_unit;
     size_t ppw = units / ((size_t)NUS_PAIRS * (size_t)cus * 2);
-    ppw = ppw < 1 ? 1 : (ppw > NUS_PPW_MAX ? NUS_PPW_MAX : ppw);
+    const size_t pmax = (size_t)(ring == NTT_RING_M32 ? nus_ppw_max<NTT_RING_M32>() : nus_ppw_max<NTT_RING_Q>());
+    ppw = ppw < 1 ? 1 : (ppw > pmax ? pmax : ppw);
     const dim3 grid((uint32_t)((units + NUS_PAIRS * ppw - 1) / (NUS_PAIRS * ppw)));
     hipStream_t s = (hipStream_t)stream;
     const uint32_t nb = (uint32_t)batch, pw = (uint32_t)ppw;

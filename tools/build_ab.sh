@@ -6,7 +6,7 @@
 set -euo pipefail
 name=$1 rev=$2; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-OUT=$ROOT/ntt-gpu-qtesla_amd/lib/ab
+OUT=${AB_OUT:-$ROOT/ntt-gpu-qtesla_amd/lib/ab}
 mkdir -p "$OUT"
 if [ "$rev" = WT ]; then
     src=$ROOT

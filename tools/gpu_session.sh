@@ -76,6 +76,12 @@ for step in "$@"; do
         sq_c*) c=${step#sq_c}; run sq_c$c 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sq_c$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-check ;;
         sqb_c*) c=${step#sqb_c}; run sqb_c$c 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM --output-format csv -d gpurun_out/sqb_c$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-check ;;
         listpmc) run listpmc 60 rocprofv3 -L ;;
+        nusstamps) run nusstamps 200 python tools/nus_stamps.py ntt-gpu-qtesla_amd/lib/diag/nus_stamps*.so ;;
+        # round 5: n > 2048 A/B (one process, interleaved) and SQ stall counters
+        abl_*) n=${step#abl_}; b=$((8589934592 / 4 / n)); run abl_$n 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param p-III-$n --batch $b --ops fwd,inv --inplace --rounds 7 ;;
+        sql_*) n=${step#sql_}; b=$((8589934592 / 4 / n)); a="--op fwdinv --param p-III-$n --batch $b --steps 2 --warmup 1 --no-cpu-baseline --no-check";
+               run sql_$n 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sql_$n -o run -- python3 bench.py $a &&
+               run sqlb_$n 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM --output-format csv -d gpurun_out/sqlb_$n -o run -- python3 bench.py $a ;;
         # VALU roofline inputs (tools/valu_summary.py): per-opcode issue cost, and
         # SQ_INSTS_VALU + GRBM_GUI_ACTIVE per launch of a config's kernel
         valucost) run valucost 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU --output-format csv -d gpurun_out/valucost -o run -- ./ntt-gpu-qtesla_amd/bin/valu_cost 16384 ;;
