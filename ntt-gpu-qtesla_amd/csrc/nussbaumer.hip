@@ -72,8 +72,8 @@ constexpr int NUS_PAIR_WORDS = 2 * NUS_MAT_WORDS;
 // units per workgroup, per ring.  Z/q: one (no table prologue to amortise;
 // 2 % faster than 16 without the prefetch, profiles/r02/s4/ab_nussbaumer_ppw.log,
 // and the prefetch does not pay there: p-III 17.68 -> 17.82 ms at 16,
-// profiles/r05/b).  Z/(2^32-1): 16 with the next unit's loads prefetched,
-// 21.89 -> 21.47 ms (p-III's n = 2048, profiles/r05/b)
+// profiles/r05/ab/ab_nus_v2_p3.log).  Z/(2^32-1): 16 with the next unit's loads prefetched,
+// 21.89 -> 21.47 ms (p-III's n = 2048, profiles/r05/ab/ab_nus_v2_p3.log)
 #ifndef NUS_PPW_Q
 #define NUS_PPW_Q 1
 #endif
