@@ -41,7 +41,6 @@ for step in "$@"; do
         cycles) run cycles 120 ./ntt-gpu-qtesla_amd/bin/valu_cycles ;;
         clock) run pmc_clock 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/pmc_clock -o run -- python3 tools/variants.py --rounds 2 ;;
         bocc) run bocc 120 ./ntt-gpu-qtesla_amd/bin/bfly_occupancy ;;
-        stamps) run stamps 200 python tools/stamps.py ;;
         copybw) run copybw 200 ./ntt-gpu-qtesla_amd/bin/copy_bw ;;
         pmcbench) run pmcb_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcb_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-check &&
                   run pmcb_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcb_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-check &&
