@@ -46,6 +46,26 @@ def test_m32_random_vs_oracle(ntt, oracle, dev, ps, batch):
     assert np.array_equal(got, oracle.m32_canon(oracle.nussbaumer(x, y, n, "m32")))
 
 
+# Z/(2^32-1) runs several units per workgroup with the next unit's words
+# loaded during the current one (csrc/nussbaumer.hip, NUS_PPW_M32): batches
+# of more than 2 units per pair slot (512 slots on 256 CUs) take that path,
+# including partial last workgroups, a half-valid last n = 1024 unit (odd
+# batch) and the in-place form (c == a; the prefetch reads the NEXT unit's a
+# before this unit's stores, which never touch it)
+@pytest.mark.parametrize("ps,batch", [("p-III", 1537), ("p-III", 4099), ("p-I", 3075), ("ref", 2049)])
+def test_m32_multi_unit_workgroups(ntt, oracle, dev, ps, batch):
+    n = _n(ps)
+    rng = np.random.default_rng(2000 + batch + n)
+    x, y = _rand_words(rng, (batch, n)), _rand_words(rng, (batch, n))
+    c = torch.empty(batch * n, dtype=torch.int32, device=dev)
+    ntt.poly_mul_nussbaumer(c, _dev(ntt, x, dev), _dev(ntt, y, dev), ps, "m32")
+    got = ntt.to_numpy_u32(c).reshape(batch, n)
+    assert np.array_equal(got, oracle.m32_canon(oracle.nussbaumer(x, y, n, "m32")))
+    da = _dev(ntt, x, dev)
+    ntt.poly_mul_nussbaumer(da, da, _dev(ntt, y, dev), ps, "m32")   # in place
+    assert np.array_equal(ntt.to_numpy_u32(da).reshape(batch, n), got)
+
+
 @pytest.mark.parametrize("n", [1024, 2048])
 def test_m32_reference_kat(ntt, dev, n):
     """test_nussbaumer (NTT.cu:1987-2005): all-ones operands -> z[k] = 2k + 2 - n mod 2^32-1"""
