@@ -602,8 +602,8 @@ def checker_legs(args, ntt_amd, torch, x, y, z, first, count, n):
     # a sampled subset of ~4096 polys plus the first and the last
     # (Nussbaumer's oracle is ~10x slower per product: 1024)
     nsamp = 1024 if args.op == "nussbaumer" else 4096
-    idx = np.unique(np.concatenate([[0, count - 1], rng.integers(0, count, nsamp - 2)])) if count > nsamp \
-        else np.arange(count)
+    idx = np.unique(np.concatenate([[0, count - 1], 1 + rng.choice(count - 2, nsamp - 2, replace=False)])) \
+        if count > nsamp else np.arange(count)
     tidx = torch.as_tensor(idx, device=x.device)
 
     def host(seed, i):   # the device generator's polys, regenerated on the host
