@@ -2,7 +2,7 @@
 # Copy one final-measurement session (tools/gpu_session.sh pytest smoke bench_c*
 # benchl_* benchm_* prof_* profl_* profm_* pmc_* pmcl_* pmcm_*) from
 # gpurun_out/ into profiles/<dest>/ and make its PMC summary the committed one
-# (profiles/pmc_summary.json, read by bench.py).   usage: tools/archive_final.sh r03/final_s2c
+# (profiles/pmc_summary.json, read by bench.py).   usage: tools/archive_final.sh r05/final
 set -euo pipefail
 D=profiles/$1
 S=gpurun_out
