@@ -143,3 +143,27 @@ def test_valu_entry_of_valu_bound_configs(ntt, config):
     assert k["SQ_INSTS_VALU"] > 1e9 and 3.0 < k["mean_simd_cycles_per_valu"] < 5.0
     assert 0.5 < k["valu_busy_at_pmc_clock"] < 1.0
     assert 1.5 < k["clock_ghz_pmc"] < 2.5
+
+
+def test_pattern_floor_skips_non_transforms_and_missing_library(monkeypatch):
+    """roofline.pattern_floor_ms is a transform-only diagnostic: product lines
+    get none, and a tree without the tools library says so instead of failing."""
+    import types
+    args = types.SimpleNamespace(op="polymul", param="p-III")
+    assert bench.pattern_floor(args, None, None, None, None, 10) is None
+
+    class _N:
+        @staticmethod
+        def param_info(p):
+            return {"n": 2048}
+    monkeypatch.setattr(bench, "DIAG_PATH", "/nonexistent/libqtesla_ntt_diag.so")
+    args = types.SimpleNamespace(op="fwdinv", param="p-III")
+    r = bench.pattern_floor(args, _N, None, None, None, 10)
+    assert "not built" in r["note"]
+    args = types.SimpleNamespace(op="fwdinv", param="p-III-8192")
+
+    class _N8:
+        @staticmethod
+        def param_info(p):
+            return {"n": 8192}
+    assert bench.pattern_floor(args, _N8, None, None, None, 10) is None   # n > 2048: no variant
