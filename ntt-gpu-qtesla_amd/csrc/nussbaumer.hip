@@ -28,7 +28,7 @@
 //                recombination (NTT.cu:272-277) exchange half a sub-polynomial
 //                set through LDS, each wave storing half of the output words.
 //   16 KiB of LDS and <= 256 VGPRs per wave -> 8 waves (2 per SIMD) per CU,
-//   one pair per workgroup.
+//   one pair per workgroup (the LDS allocation is padded to hold it there).
 //   deferred     the reference halves after every inverse butterfly (moddiv2,
 //   scaling      NTT.cu:255-258); here all 2^-L is applied once: a 32-bit
 //                rotate of `a` on load in Z/(2^32-1) (2^32 == 1); in Z/q a
@@ -61,26 +61,49 @@ namespace {
 #ifndef NUS_OCC_CFG
 #define NUS_OCC_CFG 2
 #endif
-// one pair per workgroup (32 KiB LDS), 4 workgroups per CU at <= 256 VGPRs:
-// 2 waves per SIMD; 4 pairs per 512-thread workgroup measured 1.29x slower
-// (every barrier then waits for all 8 waves, profiles/r02/ab_nussbaumer_wg.log)
+#ifndef NUS_WG_PER_CU
+#define NUS_WG_PER_CU 4
+#endif
+// one pair per workgroup (32 KiB LDS), 4 workgroups per CU: 2 waves per SIMD;
+// 4 pairs per 512-thread workgroup measured 1.29x slower (every barrier then
+// waits for all 8 waves, profiles/r02/ab_nussbaumer_wg.log).  The allocation is
+// padded to 40 KiB so that a fifth workgroup never joins a CU: the kernels
+// under 168 VGPRs (n <= 1024) would otherwise run 5 per CU, measured 6 % slower
+// (ref 7.10 -> 6.73 ms, p-I mod q 8.16 -> 7.66, mod 2^32-1 10.77 -> 10.44 at
+// 4 per CU; 3 per CU is slower again, profiles/r05/ab/ab_nus_lds_*.log).
+// Against the round-5 f06b3ab8 build (170 VGPRs at p-I mod q, so already 4 per
+// CU there): ref 7.11 -> 6.76 ms, p-I mod 2^32-1 11.11 -> 10.59, n = 2048
+// unchanged (ab_nus_lds40_*.log)
 constexpr int NUS_WG = NUS_WG_CFG;
 constexpr int NUS_WAVES = NUS_WG / 64;
 constexpr int NUS_PAIRS = NUS_WAVES / 2;
 constexpr int NUS_MAT_WORDS = 4096;             // one 64-row x R x H matrix (16 KiB)
 constexpr int NUS_PAIR_WORDS = 2 * NUS_MAT_WORDS;
+constexpr int NUS_CU_LDS_WORDS = 160 * 1024 / 4;
+// n = 2048 needs > 168 VGPRs, which caps it at 2 waves per SIMD anyway; padding
+// it too makes the compiler schedule for that occupancy and spill a VGPR
+template <int N> constexpr int nus_lds_words()
+{
+    return (N < 2048 && NUS_PAIRS * NUS_PAIR_WORDS < NUS_CU_LDS_WORDS / NUS_WG_PER_CU) ? NUS_CU_LDS_WORDS / NUS_WG_PER_CU
+                                                                                      : NUS_PAIRS * NUS_PAIR_WORDS;
+}
 // units per workgroup, per ring.  Z/q: one (no table prologue to amortise;
 // 2 % faster than 16 without the prefetch, profiles/r02/s4/ab_nussbaumer_ppw.log,
 // and the prefetch does not pay there: p-III 17.68 -> 17.82 ms at 16,
-// profiles/r05/ab/ab_nus_v2_p3.log).  Z/(2^32-1): 16 with the next unit's loads prefetched,
-// 21.89 -> 21.47 ms (p-III's n = 2048, profiles/r05/ab/ab_nus_v2_p3.log)
+// profiles/r05/ab/ab_nus_v2_p3.log).  Z/(2^32-1) at n = 2048: 16 with the next
+// unit's loads prefetched, 21.89 -> 21.47 ms (profiles/r05/ab/ab_nus_v2_p3.log);
+// at n = 1024 it does not pay (11.10 -> 11.17 ms, ab_nus_v2_p1.log) and costs
+// SGPR spills, so n = 1024 keeps one unit per workgroup
 #ifndef NUS_PPW_Q
 #define NUS_PPW_Q 1
 #endif
 #ifndef NUS_PPW_M32
 #define NUS_PPW_M32 16
 #endif
-template <int RING> constexpr int nus_ppw_max() { return RING == NTT_RING_M32 ? NUS_PPW_M32 : NUS_PPW_Q; }
+template <int PS, int RING> constexpr int nus_ppw_max()
+{
+    return (RING == NTT_RING_M32 && PSel<PS>::T::N == 2048) ? NUS_PPW_M32 : NUS_PPW_Q;
+}
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F &&f)
@@ -716,7 +739,11 @@ __device__ __forceinline__ void nus_unit(const uint32_t *a, const uint32_t *b, u
             *(uint4 *)(dst + 4 * q4) = make_uint4(o[4 * q4], o[4 * q4 + 1], o[4 * q4 + 2], o[4 * q4 + 3]);
     }
     NUS_STAMP(12, o[15] ^ o[0]);
-    if (!last) pair_sync();   // the exchange area is free for the next unit (wave-uniform, pair-uniform)
+    // the exchange area is free for the next unit (wave-uniform, pair-uniform);
+    // a one-unit-per-workgroup kernel (!PF) never has a next unit
+    if constexpr (PF) {
+        if (!last) pair_sync();
+    }
     NUS_STAMP(13, lane);
 }
 
@@ -726,10 +753,12 @@ __global__ __launch_bounds__(NUS_WG, NUS_OCC_CFG) void k_nussbaumer(const uint32
 {
     using P = typename PSel<PS>::T;
     constexpr int H = Geo<P::N>::H;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[NUS_PAIRS * NUS_PAIR_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[nus_lds_words<P::N>()];
     const uint32_t wave = threadIdx.x >> 6, pair = wave >> 1;
     uint32_t *const pl = lds + pair * NUS_PAIR_WORDS;
     const uint32_t nunits = (npoly + H - 1) / H;
+    constexpr bool PF = nus_ppw_max<PS, RING>() > 1;   // several units per workgroup: prefetch the next
+    if constexpr (!PF) ppw = 1;   // the host's cap for these kernels (nussbaumer_launch); no final barrier below
     // every pair of the workgroup runs the same number of units (idle pairs
     // past the batch still meet the barriers)
     uint32_t u = blockIdx.x * (NUS_PAIRS * ppw) + pair;
@@ -740,7 +769,6 @@ __global__ __launch_bounds__(NUS_WG, NUS_OCC_CFG) void k_nussbaumer(const uint32
     // a pair past the batch recomputes the workgroup's first unit and stores nothing
     auto unit_of = [&](uint32_t v) { return v < nunits ? v : first; };
     auto np_of = [&](uint32_t v) { return v < nunits ? npoly : 0u; };
-    constexpr bool PF = nus_ppw_max<RING>() > 1;   // several units per workgroup: prefetch the next
     uint32_t X[32], Y[32];
 #pragma unroll 1
     for (uint32_t it = 0; it < steps; ++it, u += NUS_PAIRS) {
@@ -770,7 +798,7 @@ int nussbaumer_launch(int ps, int ring, const uint32_t *a, const uint32_t *b, ui
     const size_t per_unit = ps == 2 ? 1 : 2;
     const size_t units = (batch + per_unit - 1) / per_unit;
     size_t ppw = units / ((size_t)NUS_PAIRS * (size_t)cus * 2);
-    const size_t pmax = (size_t)(ring == NTT_RING_M32 ? nus_ppw_max<NTT_RING_M32>() : nus_ppw_max<NTT_RING_Q>());
+    const size_t pmax = (size_t)((ring == NTT_RING_M32 && ps == 2) ? nus_ppw_max<2, NTT_RING_M32>() : nus_ppw_max<0, NTT_RING_Q>());
     ppw = ppw < 1 ? 1 : (ppw > pmax ? pmax : ppw);
     const dim3 grid((uint32_t)((units + NUS_PAIRS * ppw - 1) / (NUS_PAIRS * ppw)));
     hipStream_t s = (hipStream_t)stream;

@@ -38,6 +38,7 @@ for step in "$@"; do
                 run abm_p1 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param p-I --ops mul,mulntt --rounds 7 ;;
         abnus) run abn_p3 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --ops nus,nusm32 --rounds 5 &&
                run abn_p1 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param p-I --ops nus,nusm32 --rounds 5 ;;
+        abnusref) run abn_ref 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param ref --ops nus --rounds 7 ;;
         cycles) run cycles 120 ./ntt-gpu-qtesla_amd/bin/valu_cycles ;;
         clock) run pmc_clock 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/pmc_clock -o run -- python3 tools/variants.py --rounds 2 ;;
         bocc) run bocc 120 ./ntt-gpu-qtesla_amd/bin/bfly_occupancy ;;
