@@ -17,7 +17,7 @@ def main(paths):
     vals = defaultdict(lambda: defaultdict(list))
     for p in paths:
         for r in csv.DictReader(open(p)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
     for k, cs in vals.items():
