@@ -66,6 +66,10 @@ PMC_PATH = os.path.join(ROOT, "profiles", "pmc_summary.json")
 # tools-only diagnostic library (ntt-gpu-qtesla_amd/tools/ntt_diag.hip, `make tools`):
 # the transforms' memory-only variants for roofline.pattern_floor_ms
 DIAG_PATH = os.path.join(ROOT, "ntt-gpu-qtesla_amd", "lib", "libqtesla_ntt_diag.so")
+# batches of up to this many coefficients run the small-batch (latency)
+# kernels, one polynomial per workgroup (csrc/ntt_lat.hpp NTT_LAT_MAX_COEFFS /
+# NTT_LAT_MUL_MAX_COEFFS; tests/test_bench_meta.py checks they agree)
+LAT_MAX_COEFFS = 1 << 21
 
 # BASELINE.json configs -> (op, param, batch per GPU, ring)
 CONFIGS = {
@@ -305,6 +309,9 @@ def pattern_floor(args, ntt_amd, torch, x, stream, steps: int):
         return None
     if not os.path.exists(DIAG_PATH):
         return {"note": f"{os.path.relpath(DIAG_PATH, ROOT)} not built (make -C ntt-gpu-qtesla_amd tools)"}
+    if x.numel() <= LAT_MAX_COEFFS:
+        return {"note": "small batch: the latency kernels (one polynomial per workgroup, csrc/ntt_lat.hpp) run it; "
+                        "the memory-only variant is the batch kernels' and is not this launch's floor"}
     L = ctypes.CDLL(DIAG_PATH)
     vp = ctypes.c_void_p
     L.ntt_debug_variant.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
@@ -411,17 +418,17 @@ def main():
         ntt_amd.fill_uniform(y, args.param, SEED ^ 0xFFFF, first)
     stream = torch.cuda.current_stream(device)
 
-    def launch(kind):
+    def launch(kind, st=stream):
         if kind == "fwd":
-            ntt_amd.poly_ntt(x, args.param, stream)
+            ntt_amd.poly_ntt(x, args.param, st)
         elif kind == "inv":
-            ntt_amd.poly_invntt(x, args.param, stream)
+            ntt_amd.poly_invntt(x, args.param, st)
         elif kind == "mul":
-            ntt_amd.poly_mul(z, x, y, args.param, stream)
+            ntt_amd.poly_mul(z, x, y, args.param, st)
         elif kind == "mulntt":
-            ntt_amd.poly_mul_ntt(z, x, y, args.param, stream)
+            ntt_amd.poly_mul_ntt(z, x, y, args.param, st)
         else:
-            ntt_amd.poly_mul_nussbaumer(z, x, y, args.param, args.ring, stream)
+            ntt_amd.poly_mul_nussbaumer(z, x, y, args.param, args.ring, st)
 
     kinds = {"fwdinv": ["fwd", "inv"], "fwd": ["fwd"], "inv": ["inv"], "polymul": ["mul"], "polymul_ntt": ["mulntt"],
              "nussbaumer": ["nus"]}[args.op]
@@ -491,6 +498,13 @@ def main():
         check["all_ranks_ok"] = dist.max(bad) == 0.0
     if expiries is not None:
         check["slot_sync_expiries"] = expiries
+    latency = None
+    if count * n <= LAT_MAX_COEFFS and n <= 2048 and args.op != "nussbaumer":
+        try:   # beside the line, like the floor: never part of `value`
+            latency = graph_replay(torch, launch, kinds, max(args.steps, 50), device)
+        except Exception as e:   # noqa: BLE001
+            latency = {"note": f"graph replay not measured: {type(e).__name__}: {e}"}
+        latency["api_us_per_step"] = None   # filled in below from the timed region
     floor = None
     if not args.no_floor:
         try:   # a diagnostic beside the line: it must never cost the measurement itself
@@ -522,6 +536,9 @@ def main():
                         avg_launch_ms=per_kind[dom], per_kernel_ms=per_kind)
     else:
         roofline = hbm
+    if latency is not None:
+        latency["api_us_per_step"] = elapsed / args.steps * 1e6
+        roofline["latency"] = latency
     headline = args.op == "fwdinv" and args.param == "p-III" and args.batch == 1 << 20
     out = {
         "metric": METRIC if headline else f"{unit} ({workload}, batch {args.batch} per GPU)",
@@ -556,6 +573,33 @@ def main():
     dist.close()
     if (not args.no_check and not check.get("all_ranks_ok", True)) or expiries:
         sys.exit(1)
+
+
+def graph_replay(torch, launch, kinds, steps, device):
+    """Small batches are latency-bound: the timed region's rate is the Python
+    -> C ABI submission cost, not the GPU's.  Here `steps` steps are captured
+    once in a HIP graph (torch.cuda.CUDAGraph; the library's launches go to
+    the capturing stream) and replayed with an event pair around the replay:
+    the GPU time per step without host submission (kernel + launch boundary),
+    what a C caller's back-to-back loop approaches (ntt_main -speedgpu 12).
+    Never part of `value`."""
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.graph(g, stream=side):
+        for _ in range(steps):
+            for k in kinds:
+                launch(k, side)
+    g.replay()   # warm
+    torch.cuda.synchronize(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    cur = torch.cuda.current_stream(device)
+    e0.record(cur)
+    g.replay()
+    e1.record(cur)
+    torch.cuda.synchronize(device)
+    return {"graph_replay_us_per_step": e0.elapsed_time(e1) * 1e3 / steps, "graph_steps": steps,
+            "kernels": "small-batch kernels, one polynomial per n/4-thread workgroup (csrc/ntt_lat.hpp)"}
 
 
 def host_threads():

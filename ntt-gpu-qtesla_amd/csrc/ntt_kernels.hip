@@ -15,6 +15,7 @@
 #include "ntt_device.hpp"
 #include "ntt_large.hpp"
 #include "ntt_big.hpp"
+#include "ntt_lat.hpp"
 #include "ntt_internal.h"
 #include "params.hpp"
 #include "pset.hpp"
@@ -189,6 +190,16 @@ template <int PS> struct LXform {
                 inv(out, out);
                 break;
             }
+        } else if (batch * PSel<PS>::T::N <= (size_t)NTT_LAT_MAX_COEFFS && k != BITREV) {
+            // small batches: one polynomial per workgroup (ntt_lat.hpp)
+            const dim3 g((uint32_t)batch), b(PSel<PS>::T::N / 4);
+            switch (k) {
+            case FWD: hipLaunchKernelGGL((k_ntt_lat<PS, false, false>), g, b, 0, s, in, out); break;
+            case INV: hipLaunchKernelGGL((k_ntt_lat<PS, true, false>), g, b, 0, s, in, out); break;
+            case FWD_BR: hipLaunchKernelGGL((k_ntt_lat<PS, false, true>), g, b, 0, s, in, out); break;
+            case INV_BR: hipLaunchKernelGGL((k_ntt_lat<PS, true, true>), g, b, 0, s, in, out); break;
+            default: break;
+            }
         } else {
             const Launch l = launch_for(OP_XFORM, PS, batch, d);
             const dim3 g(l.grid), b(NTT_WG);
@@ -228,6 +239,12 @@ template <int PS> struct LMul {
         } else if constexpr (PS >= LARGE_PS0) {
             if (bhat) launch_mul_large<PS, true>(a, b, c, batch, s, d);
             else launch_mul_large<PS, false>(a, b, c, batch, s, d);
+            return finish_launch();
+        } else if (batch * PSel<PS>::T::N <= (size_t)NTT_LAT_MUL_MAX_COEFFS) {
+            // small batches: one product per workgroup (ntt_lat.hpp)
+            const dim3 g((uint32_t)batch), blk(PSel<PS>::T::N / 4);
+            if (bhat) hipLaunchKernelGGL((k_poly_mul_lat<PS, true>), g, blk, 0, s, a, b, c);
+            else hipLaunchKernelGGL((k_poly_mul_lat<PS, false>), g, blk, 0, s, a, b, c);
             return finish_launch();
         } else {
             if (bhat) {
@@ -452,7 +469,8 @@ int ntt_build_info(char *buf, size_t len)
     static const char *s =
         "qtesla_ntt gfx950: 1 launch/op, wave-per-poly (n=2048) / half-wave-per-poly (n=1024), 32 coeff/lane, "
         "LDS XOR-swizzled transpose, permlane32 bit-5 stage, Shoup/Harvey lazy CT + signed-Shoup GS butterflies, "
-        "dispatch-ordered unit chunks; wg=" QNTT_STR(NTT_WG)
+        "dispatch-ordered unit chunks; small batches (<= " QNTT_STR(NTT_LAT_MAX_COEFFS) " coeffs) one poly per "
+        "n/4-thread workgroup; wg=" QNTT_STR(NTT_WG)
         " mul_wg=" QNTT_STR(MUL_WG) " mul_compact=1 ppw<=" QNTT_STR(NTT_PPW_MAX)
         " min_wg/cu=" QNTT_STR(NTT_MIN_WG_PER_CU) "; src=" QNTT_SRC_HASH;
     const int n = (int)strlen(s);

@@ -1,0 +1,275 @@
+// ntt_lat.hpp -- gfx950 small-batch (latency) transforms for n = 1024 / 2048:
+// one polynomial per workgroup of n/4 threads, 4 coefficients per thread.
+//
+// Why: the qTESLA signing loop transforms one polynomial per call (BASELINE
+// config 1), and the batch kernels of ntt_device.hpp give a polynomial to one
+// wave (half a wave at n = 1024): ~1 500 VALU in one wave, which a lone wave
+// issues at one instruction per ~4 cycles (MI355X_MICROARCH.md, 'vector-
+// instruction ISSUE cost'), behind a 15.75 KiB LDS table fill and barrier.
+// Here the same butterflies are spread over n/4 lanes (4 or 8 waves, one or
+// two per SIMD), so a thread runs ~L/2 radix-4 groups (~80 VALU) and the
+// critical path is the global loads, L/2 LDS exchanges and the stores.
+//
+// Dataflow (L = log2 n, T = n/4 threads, thread t, pos bits p_{L-1}..p_0):
+//   pass j = 0 .. NP-1 runs CT stages hb = L-1-2j and lb = hb-1 on the group
+//   base(t) + {0, 2^lb, 2^hb, 2^hb + 2^lb}, base(t) = t with two zero bits
+//   inserted at lb, hb (pass 0: base = t, so the group is t + {0,T,2T,3T}, the
+//   coalesced natural-order loads).  For odd L the last pass is the lone stage
+//   on bit 0, over the group 4t + {0,1,2,3}.  Stage b's twiddle index is
+//   k = 2^(L-1-b) + (pos >> (b+1)), psi^brv(k) (the batch kernels' tables
+//   c_fwd*/c_inv*, NTT.cu:2216-2260's CT with merged twist), so stage hb uses
+//   one twiddle per group and stage lb two (k and k+1).
+//   Between passes the group values go through LDS (double-buffered, one
+//   barrier per exchange, addresses padded by one word per 32 so the strided
+//   late passes stay conflict-free); the forward's last exchange is the
+//   bit-reversal to natural order, the inverse's first the reverse.
+//   The inverse runs the passes backwards with GS butterflies (stage lb, then
+//   hb), the last stage scaled by n^-1 (and psi^-brv(1)) like the batch
+//   kernels; every twiddle is loaded from the __constant__ table up front,
+//   while the polynomial's own loads are in flight.
+// BR = true: the forward leaves X in bit-reversed order (out[t] = X[brv(t)],
+// poly_ntt_bitrev) and the inverse takes that order (poly_invntt_bitrev):
+// the reordering exchange is skipped.
+#pragma once
+#include "ntt_big.hpp"   // sfor
+
+namespace qntt {
+
+// batches of up to 2^21 coefficients (n = 2048: 1024 polynomials, n = 1024:
+// 2048) take the latency kernels: per launch in a replayed graph they run
+// 2.2 / 2.9 us at batch 1 (p-I / p-III) against 4.5 / 4.9 for the batch
+// kernels, 4.3 / 6.9 against 7.7 / 9.6 us at 1024, and lose at 2048 polys of
+// n = 2048 (11.5 against 10.9 us; profiles/r05/lat/)
+#ifndef NTT_LAT_MAX_COEFFS
+#define NTT_LAT_MAX_COEFFS 2097152   // 2^21
+#endif
+#ifndef NTT_LAT_MUL_MAX_COEFFS
+#define NTT_LAT_MUL_MAX_COEFFS 2097152   // 2^21
+#endif
+
+template <int PS, bool INV>
+__device__ __forceinline__ const uint2 *lat_tw()
+{
+    if constexpr (PS == 0) return INV ? c_inv0 : c_fwd0;
+    else if constexpr (PS == 1) return INV ? c_inv1 : c_fwd1;
+    else return INV ? c_inv2 : c_fwd2;
+}
+
+__host__ __device__ constexpr uint32_t lat_pad(uint32_t x) { return x + (x >> 5); }
+
+template <int L>
+struct LatGeo {
+    static constexpr int N = 1 << L;
+    static constexpr int T = N / 4;
+    static constexpr int NP = (L + 1) / 2;        // passes (the last one radix-2 when L is odd)
+    static constexpr int BUF = lat_pad(N - 1) + 1;   // words per exchange buffer
+    // high / low stage bit of pass j (lb < 0: the lone stage on bit 0)
+    static constexpr int hb(int j) { return L - 1 - 2 * j; }
+    static constexpr int lb(int j) { return L - 2 - 2 * j; }
+    // group layout bits of pass j: (gh, gl) = (hb, lb), or (1, 0) for the lone stage
+    static constexpr int gh(int j) { return lb(j) < 0 ? 1 : hb(j); }
+    static constexpr int gl(int j) { return lb(j) < 0 ? 0 : lb(j); }
+    // group base of thread t in pass j: t with zero bits inserted at gl and gh = gl + 1
+    static __host__ __device__ constexpr uint32_t base(int j, uint32_t t)
+    {
+        return ((t >> gl(j)) << (gh(j) + 1)) | (t & ((1u << gl(j)) - 1u));
+    }
+    // position of register e = 2 e1 + e0 of the group
+    static __host__ __device__ constexpr uint32_t pos(int j, uint32_t t, int e)
+    {
+        return base(j, t) + ((uint32_t)(e >> 1) << gh(j)) + ((uint32_t)(e & 1) << gl(j));
+    }
+};
+
+__host__ __device__ constexpr uint32_t lat_brv(uint32_t x, int bits)
+{
+    uint32_t r = 0;
+    for (int i = 0; i < bits; ++i) r |= ((x >> i) & 1u) << (bits - 1 - i);
+    return r;
+}
+
+// Every pass's twiddles of one direction for thread t (3 per radix-4 pass,
+// 2 for the lone stage), loaded up front so that their latency overlaps the
+// polynomial's own loads.
+template <int PS, bool INV>
+struct LatTw {
+    using G = LatGeo<PSel<PS>::T::LOGN>;
+    static constexpr int L = PSel<PS>::T::LOGN, NP = G::NP;
+    uint2 ta[NP], tb[NP][2];
+    __device__ __forceinline__ explicit LatTw(uint32_t t)
+    {
+        const uint2 *tw = lat_tw<PS, INV>();
+        sfor<NP>([&](auto JJ) {
+            constexpr int j = decltype(JJ)::value;
+            const uint32_t b0 = G::base(j, t);
+            if constexpr (G::lb(j) >= 0) ta[j] = tw[(1u << (L - 1 - G::hb(j))) + (b0 >> (G::hb(j) + 1))];
+            else ta[j] = make_uint2(0u, 0u);
+            const uint32_t kb = (1u << (L - 1 - G::gl(j))) + (b0 >> (G::gl(j) + 1));
+            tb[j][0] = tw[kb];
+            tb[j][1] = tw[kb + 1];
+        });
+    }
+};
+
+// LDS exchange number x of NOPS operands (buffer x & 1 of 2 x NB x BUF
+// words, NB >= NOPS fixed per kernel; consecutive exchanges alternate, so one
+// barrier each suffices): the groups go out at wmap(e), the next layout's
+// come in from rmap(e).
+template <class G, int NB, int NOPS, class WMap, class RMap>
+__device__ __forceinline__ void lat_xchg(uint32_t (&v)[NOPS][4], uint32_t *lds, int x, WMap wmap, RMap rmap)
+{
+    static_assert(NOPS <= NB, "exchange buffer too small");
+    uint32_t *buf = lds + (x & 1) * NB * G::BUF;
+#pragma unroll
+    for (int o = 0; o < NOPS; ++o)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) buf[o * G::BUF + lat_pad(wmap(e))] = v[o][e];
+    __syncthreads();
+#pragma unroll
+    for (int o = 0; o < NOPS; ++o)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[o][e] = buf[o * G::BUF + lat_pad(rmap(e))];
+}
+
+// Forward CT passes of NOPS operands (natural-order groups of pass 0 in, the
+// last pass's groups out: position pos holds X[brv(pos)], values in [0, 4q)).
+// Exchanges 0 .. NP-2.
+template <int PS, int NB, int NOPS>
+__device__ __forceinline__ void lat_fwd(uint32_t (&v)[NOPS][4], const LatTw<PS, false> &w, uint32_t *lds, uint32_t t)
+{
+    using P = typename PSel<PS>::T;
+    using G = LatGeo<P::LOGN>;
+    constexpr int NP = G::NP;
+    sfor<NP>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+#pragma unroll
+        for (int o = 0; o < NOPS; ++o) {
+            if constexpr (G::lb(j) >= 0) {
+                // stage hb; the first pass's inputs are the caller's (< 2q): no reduction
+                ct_bfly<P::Q, (j > 0)>(v[o][0], v[o][2], w.ta[j].x, w.ta[j].y);
+                ct_bfly<P::Q, (j > 0)>(v[o][1], v[o][3], w.ta[j].x, w.ta[j].y);
+            }
+            ct_bfly<P::Q>(v[o][0], v[o][1], w.tb[j][0].x, w.tb[j][0].y);
+            ct_bfly<P::Q>(v[o][2], v[o][3], w.tb[j][1].x, w.tb[j][1].y);
+        }
+        if constexpr (j + 1 < NP)
+            lat_xchg<G, NB>(v, lds, j, [&](int e) { return G::pos(j, t, e); }, [&](int e) { return G::pos(j + 1, t, e); });
+    });
+}
+
+// Inverse GS passes of one operand from the last pass's groups (inputs in
+// [0, 2q)) to the natural-order groups t + T e, the last stage scaled by S0
+// (x + y) and S1 (x - y); canonical outputs.  Exchanges x0 + 1 .. x0 + NP - 1.
+template <int PS, int NB, uint32_t S0, uint32_t S1>
+__device__ __forceinline__ void lat_inv(uint32_t (&v)[1][4], const LatTw<PS, true> &w, uint32_t *lds, uint32_t t, int x0)
+{
+    using P = typename PSel<PS>::T;
+    using G = LatGeo<P::LOGN>;
+    constexpr int NP = G::NP;
+    uint32_t(&u)[4] = v[0];
+    sfor<NP>([&](auto JJ) {
+        constexpr int j = NP - 1 - decltype(JJ)::value;
+        gs_bfly<P::Q>(u[0], u[1], w.tb[j][0].x, w.tb[j][0].y);
+        gs_bfly<P::Q>(u[2], u[3], w.tb[j][1].x, w.tb[j][1].y);
+        if constexpr (j > 0) {
+            if constexpr (G::lb(j) >= 0) {
+                gs_bfly<P::Q>(u[0], u[2], w.ta[j].x, w.ta[j].y);
+                gs_bfly<P::Q>(u[1], u[3], w.ta[j].x, w.ta[j].y);
+            }
+            lat_xchg<G, NB>(v, lds, x0 + NP - j, [&](int e) { return G::pos(j, t, e); },
+                        [&](int e) { return G::pos(j - 1, t, e); });
+        }
+    });
+    // stage L-1 (k = 1) with the scaling folded in (inv_last_stage)
+    constexpr uint32_t S0P = cshoup(S0, P::Q);
+    constexpr TwPair S1S = csigned_tw(S1, P::Q);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const uint32_t x = u[e], y = u[e + 2];
+        u[e] = csub<P::Q>(shoup_mul<P::Q>(x + y, S0, S0P));
+        u[e + 2] = csub<P::Q>(sshoup_mul<P::Q>(x - y, S1S.x, S1S.y));
+    }
+}
+
+template <int PS, bool INV, bool BR>
+__global__ __launch_bounds__(PSel<PS>::T::N / 4) void k_ntt_lat(const uint32_t *in, uint32_t *out)
+{
+    using P = typename PSel<PS>::T;
+    constexpr int L = P::LOGN;
+    using G = LatGeo<L>;
+    constexpr int T = G::T, NP = G::NP;
+    static_assert(L == 10 || L == 11, "latency kernels: n = 1024 / 2048");
+    __shared__ uint32_t lds[2 * G::BUF];
+    const uint32_t t = threadIdx.x;
+    const uint32_t *src = in + (size_t)blockIdx.x * P::N;
+    uint32_t *dst = out + (size_t)blockIdx.x * P::N;
+
+    // the polynomial's words: natural order t + T e (the inverse's
+    // bit-reversed-order input: the last forward pass's groups)
+    uint32_t v[1][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[0][e] = ld_in(src + (INV && BR ? G::pos(NP - 1, t, e) : t + T * e));
+    const LatTw<PS, INV> w(t);
+    if constexpr (!INV) {
+        lat_fwd<PS, 1>(v, w, lds, t);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[0][e] = canon4<P>(v[0][e]);
+        if constexpr (BR) {
+            // bit-reversed order is the CT's own: position pos holds X[brv(pos)]
+#pragma unroll
+            for (int e = 0; e < 4; ++e) st_out(dst + G::pos(NP - 1, t, e), v[0][e]);
+        } else {
+            lat_xchg<G, 1>(v, lds, NP - 1, [&](int e) { return lat_brv(G::pos(NP - 1, t, e), L); },
+                        [&](int e) { return t + T * e; });
+#pragma unroll
+            for (int e = 0; e < 4; ++e) st_out(dst + t + T * e, v[0][e]);
+        }
+    } else {
+        // A[pos] = X[brv(pos)]: a natural-order input reaches the last forward
+        // pass's groups through LDS (exchange 0)
+        if constexpr (!BR)
+            lat_xchg<G, 1>(v, lds, 0, [&](int e) { return lat_brv(t + T * e, L); }, [&](int e) { return G::pos(NP - 1, t, e); });
+        lat_inv<PS, 1, P::NINV, P::C1>(v, w, lds, t, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) st_out(dst + t + T * e, v[0][e]);
+    }
+}
+
+// Small-batch products c = a b mod (x^n + 1, q), one product per workgroup:
+// both forwards in the same passes (shared twiddles and barriers), the
+// pointwise Montgomery product in the forward's own bit-reversed group layout
+// (no reordering exchange either side), the inverse with n^-1 2^32 (the
+// Montgomery factor).  BHAT (poly_mul_ntt): b is already transformed, natural
+// order, so each thread reads the words of its bit-reversed positions.
+template <int PS, bool BHAT>
+__global__ __launch_bounds__(PSel<PS>::T::N / 4) void k_poly_mul_lat(const uint32_t *a, const uint32_t *b, uint32_t *c)
+{
+    using P = typename PSel<PS>::T;
+    constexpr int L = P::LOGN;
+    using G = LatGeo<L>;
+    constexpr int T = G::T, NP = G::NP, NF = BHAT ? 1 : 2;
+    static_assert(L == 10 || L == 11, "latency kernels: n = 1024 / 2048");
+    __shared__ uint32_t lds[2 * NF * G::BUF];
+    const uint32_t t = threadIdx.x;
+    const size_t off = (size_t)blockIdx.x * P::N;
+    uint32_t v[NF][4], bh[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        v[0][e] = ld_in(a + off + t + T * e);
+        if constexpr (BHAT) bh[e] = ld_in(b + off + lat_brv(G::pos(NP - 1, t, e), L));
+        else v[NF - 1][e] = ld_in(b + off + t + T * e);
+    }
+    const LatTw<PS, false> fw(t);
+    const LatTw<PS, true> iw(t);
+    lat_fwd<PS, NF>(v, fw, lds, t);
+    uint32_t z[1][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)   // a-hat, b-hat < 4q -> [0, 2q); b-hat from memory < q
+        z[0][e] = mont_mul<P>(csub<P::Q2>(v[0][e]), BHAT ? bh[e] : csub<P::Q2>(v[NF - 1][e]));
+    // the forward's last exchange was NP - 2: the inverse's first is NP - 1
+    lat_inv<PS, NF, P::NINV_R, P::C1_R>(z, iw, lds, t, NP - 2);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) st_out(c + off + t + T * e, z[0][e]);
+}
+
+}  // namespace qntt

@@ -15,6 +15,12 @@
 //                 reference's PCIe-inclusive timing region (NTT.cu:2384-2428)
 //   -speedgpu 11  Nussbaumer product on the GPU in the reference's ring
 //                 Z/(2^32-1) (test_nussbaumer, NTT.cu:1987-2005; -speedcpu 6 there)
+//   -speedgpu 12  per-call latency through the C ABI, the qTESLA signing loop's
+//                 use (one small batch per call): poly_ntt, poly_invntt and
+//                 poly_mul, each (a) called back to back (calls/s the host
+//                 sustains, HIP events around R calls) and (b) synchronised
+//                 after every call (the round trip a caller that consumes the
+//                 result sees)
 //   -param ref|p-I|p-III|p-III-4096|p-III-8192   parameter set (reference:
 //                 compile-time QTESLA set; the n = 4096 / 8192 sets run every
 //                 option but 11, whose Nussbaumer split is n <= 2048)
@@ -57,7 +63,7 @@
 
 static void help_message()
 {
-    printf("usage: ntt_main -speedgpu {4,6,7,8,9,10,11} [-param ref|p-I|p-III|p-III-4096|p-III-8192] [-batch B] [-reps R] [-r seed] [-pcie] [-debug]\n");
+    printf("usage: ntt_main -speedgpu {4,6,7,8,9,10,11,12} [-param ref|p-I|p-III|p-III-4096|p-III-8192] [-batch B] [-reps R] [-r seed] [-pcie] [-debug]\n");
 }
 
 struct Opts {
@@ -267,6 +273,73 @@ static void report_polymul(const Opts &o, const char *name, bool fused)
     }
 }
 
+// -speedgpu 12: per-call latency of the small-batch entry points.
+static int run_latency(const Opts &o)
+{
+    uint32_t n;
+    NTT_CALL(ntt_param_info(o.ps, &n, nullptr, nullptr, nullptr, nullptr, nullptr));
+    const size_t bytes = o.batch * n * 4;
+    uint32_t *d_x, *d_y, *d_z;
+    HIP_OK(hipMalloc(&d_x, bytes));
+    HIP_OK(hipMalloc(&d_y, bytes));
+    HIP_OK(hipMalloc(&d_z, bytes));
+    hipStream_t s;
+    HIP_OK(hipStreamCreate(&s));
+    NTT_CALL(ntt_fill_uniform(d_x, o.batch, o.ps, 1, 0, s));
+    NTT_CALL(ntt_fill_uniform(d_y, o.batch, o.ps, 2, 0, s));
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    const int calls = o.reps > 1 ? o.reps : 2000;
+    struct Case {
+        const char *name;
+        int (*fn)(uint32_t *, uint32_t *, uint32_t *, size_t, int, hipStream_t);
+    };
+    const Case cases[] = {
+        {"poly_ntt", [](uint32_t *x, uint32_t *, uint32_t *, size_t b, int ps, hipStream_t st) {
+             return poly_ntt(x, nullptr, b, ps, st);
+         }},
+        {"poly_invntt", [](uint32_t *x, uint32_t *, uint32_t *, size_t b, int ps, hipStream_t st) {
+             return poly_invntt(x, nullptr, b, ps, st);
+         }},
+        {"poly_mul", [](uint32_t *x, uint32_t *y, uint32_t *z, size_t b, int ps, hipStream_t st) {
+             return poly_mul(z, x, y, b, ps, st);
+         }},
+    };
+    for (const Case &c : cases) {
+        for (int w = 0; w < 50; w++) NTT_CALL(c.fn(d_x, d_y, d_z, o.batch, o.ps, s));
+        HIP_OK(hipStreamSynchronize(s));
+        // (a) back to back
+        auto t0 = std::chrono::steady_clock::now();
+        HIP_OK(hipEventRecord(e0, s));
+        for (int i = 0; i < calls; i++) NTT_CALL(c.fn(d_x, d_y, d_z, o.batch, o.ps, s));
+        HIP_OK(hipEventRecord(e1, s));
+        HIP_OK(hipEventSynchronize(e1));
+        auto t1 = std::chrono::steady_clock::now();
+        float gpu_ms = 0.f;
+        HIP_OK(hipEventElapsedTime(&gpu_ms, e0, e1));
+        const double wall_us = std::chrono::duration<double, std::micro>(t1 - t0).count() / calls;
+        // (b) synchronised after every call
+        auto t2 = std::chrono::steady_clock::now();
+        for (int i = 0; i < calls; i++) {
+            NTT_CALL(c.fn(d_x, d_y, d_z, o.batch, o.ps, s));
+            HIP_OK(hipStreamSynchronize(s));
+        }
+        auto t3 = std::chrono::steady_clock::now();
+        const double rt_us = std::chrono::duration<double, std::micro>(t3 - t2).count() / calls;
+        printf("{\"op\": \"%s\", \"n\": %u, \"batch\": %zu, \"calls\": %d, \"back_to_back_us\": %.3f, "
+               "\"gpu_events_us\": %.3f, \"round_trip_us\": %.3f}\n",
+               c.name, n, o.batch, calls, wall_us, gpu_ms * 1e3 / calls, rt_us);
+    }
+    HIP_OK(hipEventDestroy(e0));
+    HIP_OK(hipEventDestroy(e1));
+    HIP_OK(hipStreamDestroy(s));
+    HIP_OK(hipFree(d_x));
+    HIP_OK(hipFree(d_y));
+    HIP_OK(hipFree(d_z));
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     Opts o;
@@ -335,6 +408,7 @@ int main(int argc, char **argv)
         printf("all-ones KAT z[k] = 2k+2-n mod 2^32-1: %s\n", kat ? "Identical." : "Incorrect result.");
         return kat ? 0 : 1;
     }
+    case 12: return run_latency(o);
     default: help_message(); return -1;
     }
     return 0;

@@ -167,3 +167,26 @@ def test_pattern_floor_skips_non_transforms_and_missing_library(monkeypatch):
         def param_info(p):
             return {"n": 8192}
     assert bench.pattern_floor(args, _N8, None, None, None, 10) is None   # n > 2048: no variant
+
+
+def test_latency_threshold_matches_kernels(monkeypatch, tmp_path):
+    """bench.LAT_MAX_COEFFS is the library's small-batch switch
+    (csrc/ntt_lat.hpp); below it a transform line carries no pattern floor
+    (the memory-only variant is the batch kernels')."""
+    import re
+    import types
+    hdr = open(os.path.join(ROOT, "ntt-gpu-qtesla_amd", "csrc", "ntt_lat.hpp")).read()
+    for name in ("NTT_LAT_MAX_COEFFS", "NTT_LAT_MUL_MAX_COEFFS"):
+        m = re.search(rf"#define {name} (\d+)", hdr)
+        assert m and int(m.group(1)) == bench.LAT_MAX_COEFFS, name
+
+    class _N:
+        @staticmethod
+        def param_info(p):
+            return {"n": 1024}
+    lib = tmp_path / "diag.so"
+    lib.write_bytes(b"")
+    monkeypatch.setattr(bench, "DIAG_PATH", str(lib))
+    x = types.SimpleNamespace(numel=lambda: 1024)
+    r = bench.pattern_floor(types.SimpleNamespace(op="fwd", param="p-I"), _N, None, x, None, 10)
+    assert "latency kernels" in r["note"]

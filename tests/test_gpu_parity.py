@@ -60,7 +60,7 @@ def test_fwd_inv_random(ntt, oracle, dev, ps, batch):
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
-@pytest.mark.parametrize("batch", [1, 3, 130])
+@pytest.mark.parametrize("batch", [1, 3, 130, 2100])   # 2100: past the latency kernels' 2^21 coefficients
 def test_bitrev_order_transforms(ntt, oracle, dev, ps, batch):
     """poly_ntt_bitrev / poly_invntt_bitrev: the NTT domain in bit-reversed order,
     as the reference's CT-CT pipeline keeps it (bit_reverse_copy_tbl_gpu +
@@ -90,8 +90,9 @@ def test_bitrev_order_transforms(ntt, oracle, dev, ps, batch):
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
-def test_out_of_place_keeps_input(ntt, oracle, dev, ps):
-    x = oracle.fill_uniform(33, ps, 7, 0)
+@pytest.mark.parametrize("batch", [33, 2100])   # latency kernels / batch kernels
+def test_out_of_place_keeps_input(ntt, oracle, dev, ps, batch):
+    x = oracle.fill_uniform(batch, ps, 7, 0)
     tin = _dev(ntt, x, dev)
     tout = torch.empty_like(tin)
     ntt.poly_ntt_oop(tout, tin, ps)
@@ -103,7 +104,7 @@ def test_out_of_place_keeps_input(ntt, oracle, dev, ps):
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
-@pytest.mark.parametrize("batch", [1, 5, 128])
+@pytest.mark.parametrize("batch", [1, 5, 128, 2100])   # 2100: past the latency kernels' 2^21 coefficients
 def test_poly_mul_random(ntt, oracle, dev, ps, batch):
     a = oracle.fill_uniform(batch, ps, 11 + batch, 0)
     b = oracle.fill_uniform(batch, ps, 12 + batch, 0)
@@ -149,11 +150,13 @@ def test_pointwise(ntt, oracle, dev, ps):
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
-def test_edge_values(ntt, oracle, dev, ps):
+@pytest.mark.parametrize("reps", [1, 420])   # 5 / 2100 polynomials: latency kernels / batch kernels
+def test_edge_values(ntt, oracle, dev, ps, reps):
     n, q = ntt.param_info(ps)["n"], ntt.param_info(ps)["q"]
     cases = np.stack([np.zeros(n, np.uint32), np.full(n, q - 1, np.uint32),
                       np.eye(1, n, 0, dtype=np.uint32)[0], np.eye(1, n, n - 1, dtype=np.uint32)[0],
                       (np.arange(n) % 2 * (q - 1)).astype(np.uint32)])
+    cases = np.tile(cases, (reps, 1))
     t = _dev(ntt, cases, dev)
     ntt.poly_ntt(t, ps)
     assert np.array_equal(_u32(ntt, t), oracle.poly_ntt(cases, ps))
@@ -167,10 +170,11 @@ def test_edge_values(ntt, oracle, dev, ps):
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
-def test_lazy_inputs_below_2q(ntt, oracle, dev, ps):
+@pytest.mark.parametrize("batch", [4, 2100])   # latency kernels / batch kernels
+def test_lazy_inputs_below_2q(ntt, oracle, dev, ps, batch):
     """Inputs in [q, 2q) are tolerated: result == transform of (input mod q)."""
     q = ntt.param_info(ps)["q"]
-    x = oracle.fill_uniform(4, ps, 99, 0)
+    x = oracle.fill_uniform(batch, ps, 99, 0)
     xl = (x.astype(np.uint64) + q).astype(np.uint32)
     t = _dev(ntt, xl, dev)
     ntt.poly_ntt(t, ps)
@@ -281,7 +285,7 @@ def test_host_driver_kat(ps):
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
-@pytest.mark.parametrize("batch", [1, 3, 64])
+@pytest.mark.parametrize("batch", [1, 3, 64, 2100])
 def test_poly_mul_ntt_domain(ntt, oracle, dev, ps, batch):
     """poly_mul_ntt(c, a, poly_ntt(b)) == a*b mod (x^n+1, q): the CT-GS driver
     with b's forward transform done beforehand (qTESLA's NTT-domain operand)."""
