@@ -55,7 +55,8 @@ for step in "$@"; do
         # config 2's launch is ~0.11 ms: 1000 steps (0.1 s) so that the region
         # events time a steady stream of launches, not the clock ramp after idle
         # (20 / 200 / 1000 steps: 0.116 / 0.119 / 0.111 ms, profiles/r03/c2/steps.log)
-        bench_c*) c=${step#bench_c}; k=20; [ "$c" = 2 ] && k=1000; run bench_c$c 500 python bench.py --config $c --steps $k --warmup 3 --cpu-seconds 10 ;;
+        # config 1 (one polynomial per call, ~5-8 us of Python submission each) likewise
+        bench_c*) c=${step#bench_c}; k=20; [ "$c" = 2 ] || [ "$c" = 1 ] && k=1000; run bench_c$c 500 python bench.py --config $c --steps $k --warmup 3 --cpu-seconds 10 ;;
         prof_c*) c=${step#prof_c}; run prof_c$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c$c -o run -- python3 bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-check ;;
         pmc_c*) c=${step#pmc_c}; run pmc_c${c}_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_c${c}_fetch -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-check &&
                  run pmc_c${c}_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_c${c}_write -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-check &&
