@@ -282,6 +282,14 @@ def test_host_driver_kat(ps):
         r = subprocess.run([exe, "-speedgpu", opt, "-param", ps, "-batch", batch], capture_output=True, text=True,
                            timeout=120)
         assert r.returncode == 0 and "Identical." in r.stdout, r.stdout + r.stderr
+    # per-call latency option: one JSON line per entry point, small batch
+    r = subprocess.run([exe, "-speedgpu", "12", "-param", ps, "-batch", "1", "-reps", "50"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert [d["op"] for d in lines] == ["poly_ntt", "poly_invntt", "poly_mul"]
+    assert all(0 < d["back_to_back_us"] < 1e4 and d["calls"] == 50 for d in lines)
 
 
 @pytest.mark.parametrize("ps", PARAM_SETS)
