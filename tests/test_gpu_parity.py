@@ -327,3 +327,30 @@ def test_bitrev_copy(ntt, oracle, dev, ps, batch):
     assert np.array_equal(_u32(ntt, o), want)
     ntt.poly_bitrev_copy(t, t, ps)          # in place
     assert np.array_equal(_u32(ntt, t), want)
+
+
+@pytest.mark.parametrize("ps", PARAM_SETS)
+def test_latency_switch_boundary(ntt, oracle, dev, ps):
+    """The last batch the small-batch kernels take (2^21 coefficients) and the
+    first the batch kernels take give the oracle's results for every entry
+    point that switches (csrc/ntt_lat.hpp)."""
+    n = ntt.param_info(ps)["n"]
+    for batch in ((1 << 21) // n, (1 << 21) // n + 1):
+        x = oracle.fill_uniform(batch, ps, 0x51DE + batch, 0)
+        y = oracle.fill_uniform(batch, ps, 0x51DF + batch, 0)
+        X = oracle.poly_ntt(x, ps)
+        t = _dev(ntt, x, dev)
+        ntt.poly_ntt(t, ps)
+        assert np.array_equal(_u32(ntt, t), X), batch
+        ntt.poly_invntt(t, ps)
+        assert np.array_equal(_u32(ntt, t), x), batch
+        tx, ty = _dev(ntt, x, dev), _dev(ntt, y, dev)
+        tz = torch.empty_like(tx)
+        ntt.poly_mul(tz, tx, ty, ps)
+        want = oracle.poly_mul(x, y, ps)
+        assert np.array_equal(_u32(ntt, tz), want), batch
+        ntt.poly_mul_ntt(tz, tx, _dev(ntt, oracle.poly_ntt(y, ps), dev), ps)
+        assert np.array_equal(_u32(ntt, tz), want), batch
+        ntt.poly_ntt_bitrev(tz, tx, ps)
+        ntt.poly_invntt_bitrev(tz, tz, ps)
+        assert np.array_equal(_u32(ntt, tz), x), batch

@@ -70,6 +70,9 @@ def main():
             return lambda: ntt_amd.poly_invntt(x, param, cur())
         if name == "poly_mul":
             return lambda: ntt_amd.poly_mul(z, x, y, param, cur())
+        if name == "poly_ntt_ctypes":   # the C ABI straight from ctypes: the wrapper's own cost is the difference
+            L, ptr, psn = ntt_amd.lib(), x.data_ptr(), ntt_amd.PARAM_SETS[param]
+            return lambda: L.poly_ntt(ptr, None, b, psn, cur().cuda_stream)
         if name == "fwd_mem_only":
             return lambda: D.ntt_debug_variant(0, 1, y.data_ptr(), x.data_ptr(), b, ps, cur().cuda_stream)
         if name == "fwd_wg_per_poly":
@@ -79,7 +82,7 @@ def main():
     todo = []
     for b in batches:
         for param in ("p-I", "p-III"):
-            for name in ("poly_ntt", "poly_invntt", "poly_mul", "fwd_mem_only"):
+            for name in ("poly_ntt", "poly_ntt_ctypes", "poly_invntt", "poly_mul", "fwd_mem_only"):
                 todo.append((name, param, b))
             if param == "p-III":
                 todo.append(("fwd_wg_per_poly", param, b))
