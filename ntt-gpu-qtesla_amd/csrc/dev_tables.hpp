@@ -14,6 +14,7 @@
 #include "ntt_device.hpp"
 #include "ntt_large.hpp"
 #include "ntt_big.hpp"
+#include "ntt_lat.hpp"
 #include "params.hpp"
 
 namespace qntt {
@@ -211,6 +212,15 @@ inline hipError_t upload_device_tables(const Tables *tabs /* [NPARAM_SETS] */)
         hipError_t e = upload_large_tables(ps, tabs[ps]);
         if (e != hipSuccess) return e;
         if ((e = upload_big_tables(ps, tabs[ps])) != hipSuccess) return e;
+        // full n-point tables of the latency kernels (ntt_lat.hpp)
+        for (int inv = 0; inv < 2; inv++) {
+            const std::vector<uint32_t> c = dev_const_table(*param_set(ps), tabs[ps], inv != 0);
+            e = ps == LARGE_PS0 ? hipMemcpyToSymbol(HIP_SYMBOL(g_lattw3), c.data(), c.size() * 4, (size_t)inv * c.size() * 4,
+                                                    hipMemcpyHostToDevice)
+                                : hipMemcpyToSymbol(HIP_SYMBOL(g_lattw4), c.data(), c.size() * 4, (size_t)inv * c.size() * 4,
+                                                    hipMemcpyHostToDevice);
+            if (e != hipSuccess) return e;
+        }
     }
     return hipSuccess;
 }

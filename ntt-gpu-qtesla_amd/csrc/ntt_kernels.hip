@@ -165,7 +165,17 @@ enum Xform { FWD, INV, FWD_BR, INV_BR, BITREV };
 template <int PS> struct LXform {
     static int run(Xform k, const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s, const DevInfo &d)
     {
-        if constexpr (PS >= LARGE_PS0) {
+        if (batch * PSel<PS>::T::N <= (size_t)NTT_LAT_MAX_COEFFS && k != BITREV) {
+            // small batches: one polynomial per workgroup (ntt_lat.hpp)
+            const dim3 g((uint32_t)batch), b(LatGeo<PSel<PS>::T::LOGN>::T);
+            switch (k) {
+            case FWD: hipLaunchKernelGGL((k_ntt_lat<PS, false, false>), g, b, 0, s, in, out); break;
+            case INV: hipLaunchKernelGGL((k_ntt_lat<PS, true, false>), g, b, 0, s, in, out); break;
+            case FWD_BR: hipLaunchKernelGGL((k_ntt_lat<PS, false, true>), g, b, 0, s, in, out); break;
+            case INV_BR: hipLaunchKernelGGL((k_ntt_lat<PS, true, true>), g, b, 0, s, in, out); break;
+            default: break;
+            }
+        } else if constexpr (PS >= LARGE_PS0) {
             // n = 4096 / 8192: the natural-order transforms; the bit-reversed
             // orders compose them with the bit-reversal kernel (2 launches)
             const uint32_t nb = (uint32_t)batch;
@@ -189,16 +199,6 @@ template <int PS> struct LXform {
                 hipLaunchKernelGGL(k_bitrev_large<PS>, gb, bb, 0, s, in, out, nb);
                 inv(out, out);
                 break;
-            }
-        } else if (batch * PSel<PS>::T::N <= (size_t)NTT_LAT_MAX_COEFFS && k != BITREV) {
-            // small batches: one polynomial per workgroup (ntt_lat.hpp)
-            const dim3 g((uint32_t)batch), b(PSel<PS>::T::N / 4);
-            switch (k) {
-            case FWD: hipLaunchKernelGGL((k_ntt_lat<PS, false, false>), g, b, 0, s, in, out); break;
-            case INV: hipLaunchKernelGGL((k_ntt_lat<PS, true, false>), g, b, 0, s, in, out); break;
-            case FWD_BR: hipLaunchKernelGGL((k_ntt_lat<PS, false, true>), g, b, 0, s, in, out); break;
-            case INV_BR: hipLaunchKernelGGL((k_ntt_lat<PS, true, true>), g, b, 0, s, in, out); break;
-            default: break;
             }
         } else {
             const Launch l = launch_for(OP_XFORM, PS, batch, d);
@@ -227,6 +227,15 @@ template <int PS> struct LMul {
     static int run(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t batch, hipStream_t s, bool bhat,
                    const DevInfo &d)
     {
+        if constexpr (PSel<PS>::T::N <= 4096) {
+            if (batch * PSel<PS>::T::N <= (size_t)NTT_LAT_MUL_MAX_COEFFS) {
+                // small batches: one product per workgroup (ntt_lat.hpp)
+                const dim3 g((uint32_t)batch), blk(LatGeo<PSel<PS>::T::LOGN>::T);
+                if (bhat) hipLaunchKernelGGL((k_poly_mul_lat<PS, true>), g, blk, 0, s, a, b, c);
+                else hipLaunchKernelGGL((k_poly_mul_lat<PS, false>), g, blk, 0, s, a, b, c);
+                return finish_launch();
+            }
+        }
         if constexpr (PS >= LARGE_PS0 && PSel<PS>::T::N == 4096) {
             // one wave per product (ntt_big.hpp)
             const int waves = bhat ? big_mul_waves<true>() : big_mul_waves<false>();
@@ -239,12 +248,6 @@ template <int PS> struct LMul {
         } else if constexpr (PS >= LARGE_PS0) {
             if (bhat) launch_mul_large<PS, true>(a, b, c, batch, s, d);
             else launch_mul_large<PS, false>(a, b, c, batch, s, d);
-            return finish_launch();
-        } else if (batch * PSel<PS>::T::N <= (size_t)NTT_LAT_MUL_MAX_COEFFS) {
-            // small batches: one product per workgroup (ntt_lat.hpp)
-            const dim3 g((uint32_t)batch), blk(PSel<PS>::T::N / 4);
-            if (bhat) hipLaunchKernelGGL((k_poly_mul_lat<PS, true>), g, blk, 0, s, a, b, c);
-            else hipLaunchKernelGGL((k_poly_mul_lat<PS, false>), g, blk, 0, s, a, b, c);
             return finish_launch();
         } else {
             if (bhat) {

@@ -1,5 +1,6 @@
-// ntt_lat.hpp -- gfx950 small-batch (latency) transforms for n = 1024 / 2048:
-// one polynomial per workgroup of n/4 threads, 4 coefficients per thread.
+// ntt_lat.hpp -- gfx950 small-batch (latency) transforms for n = 1024 ..
+// 8192 and products for n <= 4096: one polynomial per workgroup of n/4
+// threads (n/8 at n = 8192), 4 coefficients per thread and radix-4 group.
 //
 // Why: the qTESLA signing loop transforms one polynomial per call (BASELINE
 // config 1), and the batch kernels of ntt_device.hpp give a polynomial to one
@@ -35,11 +36,13 @@
 
 namespace qntt {
 
-// batches of up to 2^21 coefficients (n = 2048: 1024 polynomials, n = 1024:
-// 2048) take the latency kernels: per launch in a replayed graph they run
-// 2.2 / 2.9 us at batch 1 (p-I / p-III) against 4.5 / 4.9 for the batch
-// kernels, 4.3 / 6.9 against 7.7 / 9.6 us at 1024, and lose at 2048 polys of
-// n = 2048 (11.5 against 10.9 us; profiles/r05/lat/)
+// batches of up to 2^21 coefficients (n = 1024 / 2048 / 4096 / 8192: 2048 /
+// 1024 / 512 / 256 polynomials) take the latency kernels: per launch in a
+// replayed graph they run 2.2 / 2.9 / 4.4 / 8.2 us at batch 1 against 4.5 /
+// 4.9 / 8.7 / 17.1 for the batch kernels, and lose at twice the switch for
+// n = 2048 (11.5 against 10.9 us at 2048 polys) and n = 8192 (36.8 against
+// 33.6 at 1024); the products (n <= 4096) switch at the same size
+// (profiles/r05/lat/)
 #ifndef NTT_LAT_MAX_COEFFS
 #define NTT_LAT_MAX_COEFFS 2097152   // 2^21
 #endif
@@ -47,21 +50,33 @@ namespace qntt {
 #define NTT_LAT_MUL_MAX_COEFFS 2097152   // 2^21
 #endif
 
+// full n-point twiddle tables of the n = 4096 / 8192 sets for the latency
+// kernels (the batch kernels there read per-chunk images), [fwd / inv][k],
+// same pairs as c_fwd* / c_inv* (dev_const_table)
+__device__ uint2 g_lattw3[2][4096];
+__device__ uint2 g_lattw4[2][8192];
+
 template <int PS, bool INV>
 __device__ __forceinline__ const uint2 *lat_tw()
 {
     if constexpr (PS == 0) return INV ? c_inv0 : c_fwd0;
     else if constexpr (PS == 1) return INV ? c_inv1 : c_fwd1;
-    else return INV ? c_inv2 : c_fwd2;
+    else if constexpr (PS == 2) return INV ? c_inv2 : c_fwd2;
+    else if constexpr (PS == 3) return g_lattw3[INV ? 1 : 0];
+    else return g_lattw4[INV ? 1 : 0];
 }
 
 __host__ __device__ constexpr uint32_t lat_pad(uint32_t x) { return x + (x >> 5); }
 
+// n/4 radix-4 groups per pass; a workgroup has at most 1024 threads, so at
+// n = 8192 each thread takes R = 2 groups, g = t and t + T
 template <int L>
 struct LatGeo {
     static constexpr int N = 1 << L;
-    static constexpr int T = N / 4;
-    static constexpr int NP = (L + 1) / 2;        // passes (the last one radix-2 when L is odd)
+    static constexpr int GN = N / 4;                 // groups per pass
+    static constexpr int R = GN > 1024 ? GN / 1024 : 1;
+    static constexpr int T = GN / R;                 // threads
+    static constexpr int NP = (L + 1) / 2;           // passes (the last one radix-2 when L is odd)
     static constexpr int BUF = lat_pad(N - 1) + 1;   // words per exchange buffer
     // high / low stage bit of pass j (lb < 0: the lone stage on bit 0)
     static constexpr int hb(int j) { return L - 1 - 2 * j; }
@@ -69,15 +84,15 @@ struct LatGeo {
     // group layout bits of pass j: (gh, gl) = (hb, lb), or (1, 0) for the lone stage
     static constexpr int gh(int j) { return lb(j) < 0 ? 1 : hb(j); }
     static constexpr int gl(int j) { return lb(j) < 0 ? 0 : lb(j); }
-    // group base of thread t in pass j: t with zero bits inserted at gl and gh = gl + 1
-    static __host__ __device__ constexpr uint32_t base(int j, uint32_t t)
+    // base of group g in pass j: g with zero bits inserted at gl and gh = gl + 1
+    static __host__ __device__ constexpr uint32_t base(int j, uint32_t g)
     {
-        return ((t >> gl(j)) << (gh(j) + 1)) | (t & ((1u << gl(j)) - 1u));
+        return ((g >> gl(j)) << (gh(j) + 1)) | (g & ((1u << gl(j)) - 1u));
     }
     // position of register e = 2 e1 + e0 of the group
-    static __host__ __device__ constexpr uint32_t pos(int j, uint32_t t, int e)
+    static __host__ __device__ constexpr uint32_t pos(int j, uint32_t g, int e)
     {
-        return base(j, t) + ((uint32_t)(e >> 1) << gh(j)) + ((uint32_t)(e & 1) << gl(j));
+        return base(j, g) + ((uint32_t)(e >> 1) << gh(j)) + ((uint32_t)(e & 1) << gl(j));
     }
 };
 
@@ -88,20 +103,20 @@ __host__ __device__ constexpr uint32_t lat_brv(uint32_t x, int bits)
     return r;
 }
 
-// Every pass's twiddles of one direction for thread t (3 per radix-4 pass,
-// 2 for the lone stage), loaded up front so that their latency overlaps the
+// Every pass's twiddles of one direction for group g (3 per radix-4 pass, 2
+// for the lone stage), loaded up front so that their latency overlaps the
 // polynomial's own loads.
 template <int PS, bool INV>
 struct LatTw {
     using G = LatGeo<PSel<PS>::T::LOGN>;
     static constexpr int L = PSel<PS>::T::LOGN, NP = G::NP;
     uint2 ta[NP], tb[NP][2];
-    __device__ __forceinline__ explicit LatTw(uint32_t t)
+    __device__ __forceinline__ void load(uint32_t g)
     {
         const uint2 *tw = lat_tw<PS, INV>();
         sfor<NP>([&](auto JJ) {
             constexpr int j = decltype(JJ)::value;
-            const uint32_t b0 = G::base(j, t);
+            const uint32_t b0 = G::base(j, g);
             if constexpr (G::lb(j) >= 0) ta[j] = tw[(1u << (L - 1 - G::hb(j))) + (b0 >> (G::hb(j) + 1))];
             else ta[j] = make_uint2(0u, 0u);
             const uint32_t kb = (1u << (L - 1 - G::gl(j))) + (b0 >> (G::gl(j) + 1));
@@ -111,31 +126,40 @@ struct LatTw {
     }
 };
 
-// LDS exchange number x of NOPS operands (buffer x & 1 of 2 x NB x BUF
-// words, NB >= NOPS fixed per kernel; consecutive exchanges alternate, so one
-// barrier each suffices): the groups go out at wmap(e), the next layout's
-// come in from rmap(e).
-template <class G, int NB, int NOPS, class WMap, class RMap>
-__device__ __forceinline__ void lat_xchg(uint32_t (&v)[NOPS][4], uint32_t *lds, int x, WMap wmap, RMap rmap)
+// A thread's groups are slots s = o R + r: operand o (a polynomial with its
+// own exchange buffer), group g = t + r T.
+template <class G>
+__device__ __forceinline__ uint32_t lat_group(uint32_t t, int s)
 {
-    static_assert(NOPS <= NB, "exchange buffer too small");
-    uint32_t *buf = lds + (x & 1) * NB * G::BUF;
-#pragma unroll
-    for (int o = 0; o < NOPS; ++o)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) buf[o * G::BUF + lat_pad(wmap(e))] = v[o][e];
-    __syncthreads();
-#pragma unroll
-    for (int o = 0; o < NOPS; ++o)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[o][e] = buf[o * G::BUF + lat_pad(rmap(e))];
+    return t + (uint32_t)(s % G::R) * G::T;
 }
 
-// Forward CT passes of NOPS operands (natural-order groups of pass 0 in, the
+// LDS exchange number x (buffer x & 1 of 2 x NB x BUF words, NB >= the
+// operands in v, fixed per kernel; consecutive exchanges alternate, so one
+// barrier each suffices): slot s's register e goes out at position wmap(g, e)
+// of its operand's buffer and comes back from rmap(g, e).
+template <class G, int NB, int NS, class WMap, class RMap>
+__device__ __forceinline__ void lat_xchg(uint32_t (&v)[NS][4], uint32_t *lds, uint32_t t, int x, WMap wmap, RMap rmap)
+{
+    static_assert(NS <= NB * G::R, "exchange buffer too small");
+    uint32_t *buf = lds + (x & 1) * NB * G::BUF;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) buf[(s / G::R) * G::BUF + lat_pad(wmap(lat_group<G>(t, s), e))] = v[s][e];
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[s][e] = buf[(s / G::R) * G::BUF + lat_pad(rmap(lat_group<G>(t, s), e))];
+}
+
+// Forward CT passes of every slot (natural-order groups of pass 0 in, the
 // last pass's groups out: position pos holds X[brv(pos)], values in [0, 4q)).
-// Exchanges 0 .. NP-2.
-template <int PS, int NB, int NOPS>
-__device__ __forceinline__ void lat_fwd(uint32_t (&v)[NOPS][4], const LatTw<PS, false> &w, uint32_t *lds, uint32_t t)
+// Exchanges 0 .. NP-2.  w[r]: the twiddles of group r.
+template <int PS, int NB, int NS>
+__device__ __forceinline__ void lat_fwd(uint32_t (&v)[NS][4], const LatTw<PS, false> (&w)[LatGeo<PSel<PS>::T::LOGN>::R],
+                                        uint32_t *lds, uint32_t t)
 {
     using P = typename PSel<PS>::T;
     using G = LatGeo<P::LOGN>;
@@ -143,95 +167,126 @@ __device__ __forceinline__ void lat_fwd(uint32_t (&v)[NOPS][4], const LatTw<PS, 
     sfor<NP>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
 #pragma unroll
-        for (int o = 0; o < NOPS; ++o) {
+        for (int s = 0; s < NS; ++s) {
+            const LatTw<PS, false> &W = w[s % G::R];
             if constexpr (G::lb(j) >= 0) {
                 // stage hb; the first pass's inputs are the caller's (< 2q): no reduction
-                ct_bfly<P::Q, (j > 0)>(v[o][0], v[o][2], w.ta[j].x, w.ta[j].y);
-                ct_bfly<P::Q, (j > 0)>(v[o][1], v[o][3], w.ta[j].x, w.ta[j].y);
+                ct_bfly<P::Q, (j > 0)>(v[s][0], v[s][2], W.ta[j].x, W.ta[j].y);
+                ct_bfly<P::Q, (j > 0)>(v[s][1], v[s][3], W.ta[j].x, W.ta[j].y);
             }
-            ct_bfly<P::Q>(v[o][0], v[o][1], w.tb[j][0].x, w.tb[j][0].y);
-            ct_bfly<P::Q>(v[o][2], v[o][3], w.tb[j][1].x, w.tb[j][1].y);
+            ct_bfly<P::Q>(v[s][0], v[s][1], W.tb[j][0].x, W.tb[j][0].y);
+            ct_bfly<P::Q>(v[s][2], v[s][3], W.tb[j][1].x, W.tb[j][1].y);
         }
         if constexpr (j + 1 < NP)
-            lat_xchg<G, NB>(v, lds, j, [&](int e) { return G::pos(j, t, e); }, [&](int e) { return G::pos(j + 1, t, e); });
+            lat_xchg<G, NB>(v, lds, t, j, [&](uint32_t g, int e) { return G::pos(j, g, e); },
+                            [&](uint32_t g, int e) { return G::pos(j + 1, g, e); });
     });
 }
 
-// Inverse GS passes of one operand from the last pass's groups (inputs in
-// [0, 2q)) to the natural-order groups t + T e, the last stage scaled by S0
-// (x + y) and S1 (x - y); canonical outputs.  Exchanges x0 + 1 .. x0 + NP - 1.
+// Inverse GS passes of one operand (R slots) from the last pass's groups
+// (inputs in [0, 2q)) to the natural-order groups g + GN e, the last stage
+// scaled by S0 (x + y) and S1 (x - y); canonical outputs.  Exchanges x0 + 1 ..
+// x0 + NP - 1.
 template <int PS, int NB, uint32_t S0, uint32_t S1>
-__device__ __forceinline__ void lat_inv(uint32_t (&v)[1][4], const LatTw<PS, true> &w, uint32_t *lds, uint32_t t, int x0)
+__device__ __forceinline__ void lat_inv(uint32_t (&v)[LatGeo<PSel<PS>::T::LOGN>::R][4],
+                                        const LatTw<PS, true> (&w)[LatGeo<PSel<PS>::T::LOGN>::R], uint32_t *lds,
+                                        uint32_t t, int x0)
 {
     using P = typename PSel<PS>::T;
     using G = LatGeo<P::LOGN>;
     constexpr int NP = G::NP;
-    uint32_t(&u)[4] = v[0];
     sfor<NP>([&](auto JJ) {
         constexpr int j = NP - 1 - decltype(JJ)::value;
-        gs_bfly<P::Q>(u[0], u[1], w.tb[j][0].x, w.tb[j][0].y);
-        gs_bfly<P::Q>(u[2], u[3], w.tb[j][1].x, w.tb[j][1].y);
-        if constexpr (j > 0) {
-            if constexpr (G::lb(j) >= 0) {
-                gs_bfly<P::Q>(u[0], u[2], w.ta[j].x, w.ta[j].y);
-                gs_bfly<P::Q>(u[1], u[3], w.ta[j].x, w.ta[j].y);
+#pragma unroll
+        for (int r = 0; r < G::R; ++r) {
+            uint32_t(&u)[4] = v[r];
+            gs_bfly<P::Q>(u[0], u[1], w[r].tb[j][0].x, w[r].tb[j][0].y);
+            gs_bfly<P::Q>(u[2], u[3], w[r].tb[j][1].x, w[r].tb[j][1].y);
+            if constexpr (j > 0 && G::lb(j) >= 0) {
+                gs_bfly<P::Q>(u[0], u[2], w[r].ta[j].x, w[r].ta[j].y);
+                gs_bfly<P::Q>(u[1], u[3], w[r].ta[j].x, w[r].ta[j].y);
             }
-            lat_xchg<G, NB>(v, lds, x0 + NP - j, [&](int e) { return G::pos(j, t, e); },
-                        [&](int e) { return G::pos(j - 1, t, e); });
         }
+        if constexpr (j > 0)
+            lat_xchg<G, NB>(v, lds, t, x0 + NP - j, [&](uint32_t g, int e) { return G::pos(j, g, e); },
+                            [&](uint32_t g, int e) { return G::pos(j - 1, g, e); });
     });
     // stage L-1 (k = 1) with the scaling folded in (inv_last_stage)
     constexpr uint32_t S0P = cshoup(S0, P::Q);
     constexpr TwPair S1S = csigned_tw(S1, P::Q);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        const uint32_t x = u[e], y = u[e + 2];
-        u[e] = csub<P::Q>(shoup_mul<P::Q>(x + y, S0, S0P));
-        u[e + 2] = csub<P::Q>(sshoup_mul<P::Q>(x - y, S1S.x, S1S.y));
-    }
+    for (int r = 0; r < G::R; ++r)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const uint32_t x = v[r][e], y = v[r][e + 2];
+            v[r][e] = csub<P::Q>(shoup_mul<P::Q>(x + y, S0, S0P));
+            v[r][e + 2] = csub<P::Q>(sshoup_mul<P::Q>(x - y, S1S.x, S1S.y));
+        }
+}
+
+template <int PS, bool INV>
+__device__ __forceinline__ void lat_tws(LatTw<PS, INV> (&w)[LatGeo<PSel<PS>::T::LOGN>::R], uint32_t t)
+{
+    using G = LatGeo<PSel<PS>::T::LOGN>;
+#pragma unroll
+    for (int r = 0; r < G::R; ++r) w[r].load(t + (uint32_t)r * G::T);
 }
 
 template <int PS, bool INV, bool BR>
-__global__ __launch_bounds__(PSel<PS>::T::N / 4) void k_ntt_lat(const uint32_t *in, uint32_t *out)
+__global__ __launch_bounds__(LatGeo<PSel<PS>::T::LOGN>::T) void k_ntt_lat(const uint32_t *in, uint32_t *out)
 {
     using P = typename PSel<PS>::T;
     constexpr int L = P::LOGN;
     using G = LatGeo<L>;
-    constexpr int T = G::T, NP = G::NP;
-    static_assert(L == 10 || L == 11, "latency kernels: n = 1024 / 2048");
+    constexpr int GN = G::GN, NP = G::NP, R = G::R;
     __shared__ uint32_t lds[2 * G::BUF];
     const uint32_t t = threadIdx.x;
     const uint32_t *src = in + (size_t)blockIdx.x * P::N;
     uint32_t *dst = out + (size_t)blockIdx.x * P::N;
 
-    // the polynomial's words: natural order t + T e (the inverse's
+    // the polynomial's words: natural order g + GN e (the inverse's
     // bit-reversed-order input: the last forward pass's groups)
-    uint32_t v[1][4];
+    uint32_t v[R][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[0][e] = ld_in(src + (INV && BR ? G::pos(NP - 1, t, e) : t + T * e));
-    const LatTw<PS, INV> w(t);
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t g = t + (uint32_t)r * G::T;
+            v[r][e] = ld_in(src + (INV && BR ? G::pos(NP - 1, g, e) : g + GN * e));
+        }
+    LatTw<PS, INV> w[R];
+    lat_tws<PS, INV>(w, t);
     if constexpr (!INV) {
         lat_fwd<PS, 1>(v, w, lds, t);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[0][e] = canon4<P>(v[0][e]);
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[r][e] = canon4<P>(v[r][e]);
         if constexpr (BR) {
             // bit-reversed order is the CT's own: position pos holds X[brv(pos)]
 #pragma unroll
-            for (int e = 0; e < 4; ++e) st_out(dst + G::pos(NP - 1, t, e), v[0][e]);
-        } else {
-            lat_xchg<G, 1>(v, lds, NP - 1, [&](int e) { return lat_brv(G::pos(NP - 1, t, e), L); },
-                        [&](int e) { return t + T * e; });
+            for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) st_out(dst + t + T * e, v[0][e]);
+                for (int e = 0; e < 4; ++e) st_out(dst + G::pos(NP - 1, t + (uint32_t)r * G::T, e), v[r][e]);
+        } else {
+            lat_xchg<G, 1>(v, lds, t, NP - 1, [&](uint32_t g, int e) { return lat_brv(G::pos(NP - 1, g, e), L); },
+                           [&](uint32_t g, int e) { return g + GN * e; });
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) st_out(dst + t + (uint32_t)r * G::T + GN * e, v[r][e]);
         }
     } else {
         // A[pos] = X[brv(pos)]: a natural-order input reaches the last forward
         // pass's groups through LDS (exchange 0)
         if constexpr (!BR)
-            lat_xchg<G, 1>(v, lds, 0, [&](int e) { return lat_brv(t + T * e, L); }, [&](int e) { return G::pos(NP - 1, t, e); });
+            lat_xchg<G, 1>(v, lds, t, 0, [&](uint32_t g, int e) { return lat_brv(g + GN * e, L); },
+                           [&](uint32_t g, int e) { return G::pos(NP - 1, g, e); });
         lat_inv<PS, 1, P::NINV, P::C1>(v, w, lds, t, 0);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) st_out(dst + t + T * e, v[0][e]);
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) st_out(dst + t + (uint32_t)r * G::T + GN * e, v[r][e]);
     }
 }
 
@@ -241,26 +296,29 @@ __global__ __launch_bounds__(PSel<PS>::T::N / 4) void k_ntt_lat(const uint32_t *
 // (no reordering exchange either side), the inverse with n^-1 2^32 (the
 // Montgomery factor).  BHAT (poly_mul_ntt): b is already transformed, natural
 // order, so each thread reads the words of its bit-reversed positions.
+// n <= 4096 (one group per thread: both directions' twiddles stay in VGPRs).
 template <int PS, bool BHAT>
-__global__ __launch_bounds__(PSel<PS>::T::N / 4) void k_poly_mul_lat(const uint32_t *a, const uint32_t *b, uint32_t *c)
+__global__ __launch_bounds__(LatGeo<PSel<PS>::T::LOGN>::T) void k_poly_mul_lat(const uint32_t *a, const uint32_t *b, uint32_t *c)
 {
     using P = typename PSel<PS>::T;
     constexpr int L = P::LOGN;
     using G = LatGeo<L>;
-    constexpr int T = G::T, NP = G::NP, NF = BHAT ? 1 : 2;
-    static_assert(L == 10 || L == 11, "latency kernels: n = 1024 / 2048");
+    static_assert(G::R == 1, "latency products: n <= 4096");
+    constexpr int GN = G::GN, NP = G::NP, NF = BHAT ? 1 : 2;
     __shared__ uint32_t lds[2 * NF * G::BUF];
     const uint32_t t = threadIdx.x;
     const size_t off = (size_t)blockIdx.x * P::N;
     uint32_t v[NF][4], bh[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        v[0][e] = ld_in(a + off + t + T * e);
+        v[0][e] = ld_in(a + off + t + GN * e);
         if constexpr (BHAT) bh[e] = ld_in(b + off + lat_brv(G::pos(NP - 1, t, e), L));
-        else v[NF - 1][e] = ld_in(b + off + t + T * e);
+        else v[NF - 1][e] = ld_in(b + off + t + GN * e);
     }
-    const LatTw<PS, false> fw(t);
-    const LatTw<PS, true> iw(t);
+    LatTw<PS, false> fw[1];
+    LatTw<PS, true> iw[1];
+    lat_tws<PS, false>(fw, t);
+    lat_tws<PS, true>(iw, t);
     lat_fwd<PS, NF>(v, fw, lds, t);
     uint32_t z[1][4];
 #pragma unroll
@@ -269,7 +327,7 @@ __global__ __launch_bounds__(PSel<PS>::T::N / 4) void k_poly_mul_lat(const uint3
     // the forward's last exchange was NP - 2: the inverse's first is NP - 1
     lat_inv<PS, NF, P::NINV_R, P::C1_R>(z, iw, lds, t, NP - 2);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) st_out(c + off + t + T * e, z[0][e]);
+    for (int e = 0; e < 4; ++e) st_out(c + off + t + GN * e, z[0][e]);
 }
 
 }  // namespace qntt

@@ -37,17 +37,19 @@ def test_large_fwd_inv_random(ntt, oracle, dev, ps, batch):
 
 
 @pytest.mark.parametrize("ps", LARGE_SETS)
-def test_large_edge_values_and_lazy_inputs(ntt, oracle, dev, ps):
+@pytest.mark.parametrize("reps", [1, 100])   # 6 / 600 polynomials: latency kernels / batch kernels
+def test_large_edge_values_and_lazy_inputs(ntt, oracle, dev, ps, reps):
     n, q = ntt.param_info(ps)["n"], ntt.param_info(ps)["q"]
     cases = np.stack([np.zeros(n, np.uint32), np.full(n, q - 1, np.uint32),
                       np.eye(1, n, 0, dtype=np.uint32)[0], np.eye(1, n, n - 1, dtype=np.uint32)[0],
                       np.eye(1, n, n // 2, dtype=np.uint32)[0], (np.arange(n) % 2 * (q - 1)).astype(np.uint32)])
+    cases = np.tile(cases, (reps, 1))
     for fwd in (True, False):
         t = _dev(ntt, cases, dev)
         (ntt.poly_ntt if fwd else ntt.poly_invntt)(t, ps)
         want = oracle.poly_ntt(cases, ps) if fwd else oracle.poly_invntt(cases, ps)
         assert np.array_equal(_u32(ntt, t), want)
-    x = oracle.fill_uniform(3, ps, 77, 0)
+    x = oracle.fill_uniform(3 * reps, ps, 77, 0)
     xl = (x.astype(np.uint64) + q).astype(np.uint32)   # inputs in [q, 2q)
     t = _dev(ntt, xl, dev)
     ntt.poly_ntt(t, ps)
@@ -58,10 +60,12 @@ def test_large_edge_values_and_lazy_inputs(ntt, oracle, dev, ps):
 
 
 @pytest.mark.parametrize("ps", LARGE_SETS)
-def test_large_out_of_place_and_pattern(ntt, oracle, dev, ps):
+@pytest.mark.parametrize("reps", [1, 600])   # latency kernels / batch kernels
+def test_large_out_of_place_and_pattern(ntt, oracle, dev, ps, reps):
     n = ntt.param_info(ps)["n"]
     pat = np.zeros((1, n), np.uint32)
     pat[0, : n // 2] = n // 2 - np.arange(n // 2)   # init_operand (NTT.cu:10-15)
+    pat = np.tile(pat, (reps, 1))
     a = _dev(ntt, pat, dev)
     b = torch.empty_like(a)
     ntt.poly_ntt_oop(b, a, ps)
@@ -106,10 +110,11 @@ def test_large_nussbaumer_unsupported(ntt, dev):
 
 
 @pytest.mark.parametrize("ps", LARGE_SETS)
-@pytest.mark.parametrize("batch", [1, 2, 5, 7, 64, 389])
+@pytest.mark.parametrize("batch", [1, 2, 5, 7, 64, 389, 600])
 def test_large_poly_mul_random(ntt, oracle, dev, ps, batch):
     """Fused products, bit-exact against the oracle, over partial and full
-    workgroup steps: n = 4096 on k_poly_mul_big (one wave per product, 8 per
+    workgroup steps: n = 4096 up to 512 products on the latency kernel
+    (ntt_lat.hpp), 600 on k_poly_mul_big (one wave per product, 8 per
     workgroup), n = 8192 on k_poly_mul_large (poly_mul: 4 products per step on
     8-wave workgroups; poly_mul_ntt: 8 on 16-wave ones) -- 5, 7 and 389 are
     multiples of none of them."""
@@ -184,7 +189,7 @@ def test_large_bit_reversed_orders(ntt, oracle, dev, ps):
     log2 n = 12 / 13 bits, in and out of place; poly_ntt_bitrev =
     bitrev(poly_ntt); poly_invntt_bitrev on bit-reversed input = the CT
     inverse (oracle_poly_invntt_ct) = poly_invntt."""
-    for batch in (1, 3, 130):
+    for batch in (1, 3, 130, 600):   # 600: past the latency kernels' 2^21 coefficients
         x = oracle.fill_uniform(batch, ps, 0xB17 + batch, 0)
         tx = _dev(ntt, x, dev)
         ty = torch.empty_like(tx)

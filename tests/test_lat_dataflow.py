@@ -4,7 +4,7 @@ threads, 4 coefficients per thread): the pass groups tile every position
 exactly once, the padded LDS exchange addresses stay inside one buffer, and
 the dataflow -- the kernel's passes, twiddle indices and exchanges run with
 exact arithmetic mod q -- equals the oracle's forward and inverse for n = 1024
-(ref, p-I) and n = 2048 (p-III), in natural and bit-reversed order."""
+(ref, p-I), 2048 (p-III) and 4096 / 8192, in natural and bit-reversed order."""
 import numpy as np
 import pytest
 
@@ -17,8 +17,11 @@ class Geo:
     """LatGeo<L> of ntt_lat.hpp."""
 
     def __init__(self, L):
+        # T here counts groups (GN of the kernel); the kernel's threads take
+        # R = GN / 1024 groups each at n = 8192, which changes no position
         self.L, self.N, self.T, self.NP = L, 1 << L, 1 << (L - 2), (L + 1) // 2
         self.BUF = self.pad(self.N - 1) + 1
+        self.R = max(1, self.T // 1024)
 
     @staticmethod
     def pad(x):
@@ -37,10 +40,10 @@ class Geo:
         return self.base(j, t) + ((e >> 1) << self.gh(j)) + ((e & 1) << self.gl(j))
 
 
-PARAMS = [("ref", 10), ("p-I", 10), ("p-III", 11)]
+PARAMS = [("ref", 10), ("p-I", 10), ("p-III", 11), ("p-III-4096", 12), ("p-III-8192", 13)]
 
 
-@pytest.mark.parametrize("L", [10, 11])
+@pytest.mark.parametrize("L", [10, 11, 12, 13])
 def test_groups_tile_and_pad(L):
     G = Geo(L)
     for j in range(G.NP):
@@ -50,6 +53,7 @@ def test_groups_tile_and_pad(L):
             assert all(G.pos(0, t, e) == t + G.T * e for t in range(G.T) for e in range(4))
     pads = {G.pad(p) for p in range(G.N)}
     assert len(pads) == G.N and max(pads) < G.BUF
+    assert G.T // G.R <= 1024                  # threads per workgroup
     # stage-lb twiddle pairs: the second pair's index is the first's + 1
     for j in range(G.NP):
         for t in range(G.T):
@@ -154,7 +158,7 @@ def test_lat_dataflow_matches_oracle(oracle, param, L):
     assert np.array_equal(lat_inverse(Xb, q, L, itw, ninv, br=True), x.astype(np.int64))
 
 
-@pytest.mark.parametrize("param,L", PARAMS)
+@pytest.mark.parametrize("param,L", PARAMS[:4])   # the product kernels stop at n = 4096
 def test_lat_product_dataflow(oracle, param, L):
     """k_poly_mul_lat: both forwards left in the CT's bit-reversed group
     order, the pointwise product there (the kernel's Montgomery 2^-32 is undone

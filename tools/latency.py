@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--lib", default=None, help="product library to load instead of the in-tree one")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--params", default="p-I,p-III")
     args = ap.parse_args()
     if args.lib:
         os.environ["NTT_AMD_LIB"] = args.lib
@@ -51,7 +52,8 @@ def main():
     s = torch.cuda.current_stream()
     batches = [int(b) for b in args.batches.split(",")]
     bufs = {}
-    for param in ("p-I", "p-III"):
+    params = args.params.split(",")
+    for param in params:
         n = ntt_amd.param_info(param)["n"]
         for b in batches:
             x = torch.empty(b * n, dtype=torch.int32, device="cuda")
@@ -81,8 +83,10 @@ def main():
 
     todo = []
     for b in batches:
-        for param in ("p-I", "p-III"):
+        for param in params:
             for name in ("poly_ntt", "poly_ntt_ctypes", "poly_invntt", "poly_mul", "fwd_mem_only"):
+                if name == "fwd_mem_only" and ntt_amd.param_info(param)["n"] > 2048:
+                    continue   # the diagnostic variants are n <= 2048
                 todo.append((name, param, b))
             if param == "p-III":
                 todo.append(("fwd_wg_per_poly", param, b))
