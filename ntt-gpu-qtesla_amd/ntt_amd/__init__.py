@@ -181,13 +181,26 @@ def raw_poly_mul(c: int, a: int, b: int, batch: int, param_set, stream=None):
 
 # ------------------------------------------------------------- torch API
 
+_TORCH = None
+_INT_DTYPES = ()
+
+
 def _torch():
-    import torch
-    return torch
+    """torch, imported on first use (this module also serves torch-free
+    ctypes callers) and then cached: the per-call wrappers below run once per
+    polynomial in the signing loop's small calls."""
+    global _TORCH, _INT_DTYPES
+    if _TORCH is None:
+        import torch
+        _INT_DTYPES = (torch.int32, getattr(torch, "uint32", torch.int32))
+        _TORCH = torch
+    return _TORCH
 
 
 def _device_of(*tensors):
     """The one device all operands live on (ValueError otherwise)."""
+    if len(tensors) == 1 and getattr(tensors[0], "is_cuda", False):
+        return tensors[0].device
     dev = None
     for t in tensors:
         if not getattr(t, "is_cuda", False):
@@ -200,29 +213,29 @@ def _device_of(*tensors):
 
 
 def _stream(stream, device=None):
-    torch = _torch()
     if stream is None:
-        return torch.cuda.current_stream(device).cuda_stream
-    return stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        return _torch().cuda.current_stream(device).cuda_stream
+    return getattr(stream, "cuda_stream", stream)
 
 
 def _batch(t, n: int) -> int:
-    torch = _torch()
+    _torch()
     if not t.is_cuda:
         raise ValueError("ntt_amd operates on device tensors only (no CPU fallback)")
-    if t.dtype not in (torch.int32, getattr(torch, "uint32", torch.int32)):
+    if t.dtype not in _INT_DTYPES:
         raise TypeError(f"expected int32/uint32 storage, got {t.dtype}")
     if not t.is_contiguous():
         raise ValueError("tensor must be contiguous (poly-major [batch][n])")
-    if t.numel() % n:
-        raise ValueError(f"numel {t.numel()} is not a multiple of n={n}")
-    return t.numel() // n
+    numel = t.numel()
+    if numel % n:
+        raise ValueError(f"numel {numel} is not a multiple of n={n}")
+    return numel // n
 
 
 def _run(where: str, tensors, stream, call):
     """Check the operands, make their device current and call `call(stream)`."""
     dev = _device_of(*tensors)
-    torch = _torch()
+    torch = _TORCH or _torch()
     if torch.cuda.current_device() == dev.index:   # already current: no device switch
         _check(call(_stream(stream, dev)), where)
         return
