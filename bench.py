@@ -538,6 +538,8 @@ def main():
         roofline = hbm
     if latency is not None:
         latency["api_us_per_step"] = elapsed / args.steps * 1e6
+        if rank == 0 and world == 1 and args.op in ("fwd", "inv", "polymul"):
+            latency.update(native_latency(args, count))
         roofline["latency"] = latency
     headline = args.op == "fwdinv" and args.param == "p-III" and args.batch == 1 << 20
     out = {
@@ -600,6 +602,29 @@ def graph_replay(torch, launch, kinds, steps, device):
     torch.cuda.synchronize(device)
     return {"graph_replay_us_per_step": e0.elapsed_time(e1) * 1e3 / steps, "graph_steps": steps,
             "kernels": "small-batch kernels, one polynomial per n/4-thread workgroup (csrc/ntt_lat.hpp)"}
+
+
+def native_latency(args, batch):
+    """The same calls from C++ through the C ABI, back to back on one stream
+    (`ntt_main -speedgpu 12`, a child process): what the qTESLA signing loop,
+    a C program, pays per call without Python's submission cost.  Beside the
+    line, never part of `value`; a failure is reported, not raised."""
+    import subprocess
+    exe = os.path.join(ROOT, "ntt-gpu-qtesla_amd", "bin", "ntt_main")
+    op = {"fwd": "poly_ntt", "inv": "poly_invntt", "polymul": "poly_mul"}[args.op]
+    try:
+        r = subprocess.run([exe, "-speedgpu", "12", "-param", args.param, "-batch", str(batch), "-reps", "2000"],
+                           capture_output=True, text=True, timeout=120)
+        for line in r.stdout.splitlines():
+            if line.startswith("{") and json.loads(line).get("op") == op:
+                d = json.loads(line)
+                return {"native_c_abi_us_per_call": d["back_to_back_us"],
+                        "native_round_trip_us": d["round_trip_us"],
+                        "native_note": "ntt_main -speedgpu 12: 2000 calls back to back on one stream "
+                                       "(round trip: a stream synchronisation after every call)"}
+        return {"native_note": f"ntt_main -speedgpu 12 gave no {op} line (rc {r.returncode})"}
+    except Exception as e:   # noqa: BLE001
+        return {"native_note": f"ntt_main -speedgpu 12 not run: {type(e).__name__}: {e}"}
 
 
 def host_threads():
