@@ -66,10 +66,16 @@ PMC_PATH = os.path.join(ROOT, "profiles", "pmc_summary.json")
 # tools-only diagnostic library (ntt-gpu-qtesla_amd/tools/ntt_diag.hip, `make tools`):
 # the transforms' memory-only variants for roofline.pattern_floor_ms
 DIAG_PATH = os.path.join(ROOT, "ntt-gpu-qtesla_amd", "lib", "libqtesla_ntt_diag.so")
-# batches of up to this many coefficients run the small-batch (latency)
-# kernels, one polynomial per workgroup (csrc/ntt_lat.hpp NTT_LAT_MAX_COEFFS /
-# NTT_LAT_MUL_MAX_COEFFS; tests/test_bench_meta.py checks they agree)
-LAT_MAX_COEFFS = 1 << 21
+# the library's small-batch switch entry points of each bench op
+# (ntt_small_batch_max, csrc/ntt_lat.hpp: one threshold per (n, op))
+SWITCH_OPS = {"fwd": ["fwd"], "inv": ["inv"], "fwdinv": ["fwd", "inv"], "polymul": ["mul"],
+              "polymul_ntt": ["mul_ntt"], "nussbaumer": []}
+
+
+def runs_latency_kernels(ntt_amd, op: str, param: str, batch: int) -> bool:
+    """True when some launch of a step of `op` at `batch` polynomials runs
+    the small-batch kernels (one polynomial per workgroup, csrc/ntt_lat.hpp)."""
+    return any(batch <= ntt_amd.small_batch_max(param, k) for k in SWITCH_OPS[op])
 
 # BASELINE.json configs -> (op, param, batch per GPU, ring)
 CONFIGS = {
@@ -309,7 +315,7 @@ def pattern_floor(args, ntt_amd, torch, x, stream, steps: int):
         return None
     if not os.path.exists(DIAG_PATH):
         return {"note": f"{os.path.relpath(DIAG_PATH, ROOT)} not built (make -C ntt-gpu-qtesla_amd tools)"}
-    if x.numel() <= LAT_MAX_COEFFS:
+    if runs_latency_kernels(ntt_amd, args.op, args.param, x.numel() // ntt_amd.param_info(args.param)["n"]):
         return {"note": "small batch: the latency kernels (one polynomial per workgroup, csrc/ntt_lat.hpp) run it; "
                         "the memory-only variant is the batch kernels' and is not this launch's floor"}
     L = ctypes.CDLL(DIAG_PATH)
@@ -499,7 +505,7 @@ def main():
     if expiries is not None:
         check["slot_sync_expiries"] = expiries
     latency = None
-    if count * n <= LAT_MAX_COEFFS and n <= 2048 and args.op != "nussbaumer":
+    if runs_latency_kernels(ntt_amd, args.op, args.param, count) and n <= 2048:
         try:   # beside the line, like the floor: never part of `value`
             latency = graph_replay(torch, launch, kinds, max(args.steps, 50), device)
         except Exception as e:   # noqa: BLE001

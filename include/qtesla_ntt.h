@@ -44,9 +44,8 @@ extern "C" {
  * per polynomial (the n = 8192 products: a multi-wave four-step kernel).
  * For these sets every entry point is accepted except
  * poly_mul_nussbaumer (NTT_ERR_PARAM: its split is defined for n = 1024 /
- * 2048).  poly_mul / poly_mul_ntt are one fused launch; poly_bitrev_copy is
- * one launch; poly_ntt_bitrev / poly_invntt_bitrev are two (the natural-order
- * transform and the bit-reversal, in that / the opposite order). */
+ * 2048).  poly_mul / poly_mul_ntt are one fused launch; poly_bitrev_copy,
+ * poly_ntt_bitrev and poly_invntt_bitrev are one launch each. */
 #define NTT_PARAM_N4096 3 /* n = 4096, q = 856145921, psi = 3^((q-1)/2n)    */
 #define NTT_PARAM_N8192 4 /* n = 8192, q = 856145921, psi = 3^((q-1)/2n)    */
 
@@ -201,6 +200,20 @@ const char *ntt_strerror(int code);
  * wave per polynomial and has none).  Always 0 unless the hardware schedule
  * broke the barrier; a launch that raised it produced invalid output. */
 int ntt_sync_expiries(uint32_t *count);
+
+/* Small-batch switch: writes to *max_batch the largest batch for which
+ * entry point `op` (NTT_OP_*) of `param_set` runs the small-batch kernels
+ * (one polynomial per workgroup; 0 = never); larger batches
+ * run the batch kernels.  Both give identical results; the threshold is the
+ * measured crossover of their launch times, one per (n, op).  The reference
+ * has one launch shape for every batch (<<<BATCH, T>>>, NTT.cu:2216). */
+#define NTT_OP_FWD 0     /* poly_ntt, poly_ntt_oop       */
+#define NTT_OP_INV 1     /* poly_invntt, poly_invntt_oop */
+#define NTT_OP_FWD_BR 2  /* poly_ntt_bitrev              */
+#define NTT_OP_INV_BR 3  /* poly_invntt_bitrev           */
+#define NTT_OP_MUL 4     /* poly_mul                     */
+#define NTT_OP_MUL_NTT 5 /* poly_mul_ntt                 */
+int ntt_small_batch_max(int param_set, int op, size_t *max_batch);
 
 /* Library / kernel description for reports, ending in "src=<16 hex>" (a hash
  * of the library sources): writes at most len bytes, returns the length. */

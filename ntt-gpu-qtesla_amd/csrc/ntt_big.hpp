@@ -100,6 +100,9 @@ struct Big {
     static_assert(LDS_WORDS * 4 <= 160 * 1024, "one workgroup per CU");
     // register of transposition row t of chunk c (layout A'')
     static __host__ __device__ constexpr int creg(int c, int t) { return (c >> 1) + (1 << (NC - 1)) * t + H * (c & 1); }
+    // word offset of A'' register j from the lane's base (l & 31) + 2^(L-1) (l >> 5):
+    // pos 6..L-2 = register bits 0..M-2, pos 5 = register bit M-1
+    static __host__ __device__ constexpr uint32_t aoff(int j) { return ((uint32_t)(j & (H - 1)) << 6) | ((uint32_t)(j >> (M - 1)) << 5); }
     // word offset of B register j' of chunk c from the lane's natural-order base
     static __host__ __device__ constexpr uint32_t boff(int c, int jp)
     {
@@ -331,7 +334,21 @@ __device__ __forceinline__ void big_load_b(uint32_t (&r)[BG::R], const uint32_t 
     sfor<BG::CH>([&](auto C) { sfor<32>([&](auto JP) { r[BG::creg(C, JP)] = ld_in(src + lo + BG::boff(C, JP)); }); });
 }
 
-template <int PS>
+// layout A'' words at their own positions: the bit-reversed NTT-domain order
+// (position pos holds X[brv(pos)]), two 128-B runs per instruction
+template <class BG>
+__device__ __forceinline__ uint32_t big_a2_lane(uint32_t lane)
+{
+    uint32_t lo = (lane & 31u) + ((lane >> 5) << (BG::L - 1));
+    asm volatile("" : "+v"(lo));
+    return lo;
+}
+
+// Forward, natural-order input.  BR = false: natural-order output (layout B
+// stores); BR = true (poly_ntt_bitrev): out[t] = X[brv(t)] in one launch --
+// after pass 2 each chunk goes back through the wave's LDS buffer to layout
+// A'' (the inverse's transpose) and is stored at its own positions.
+template <int PS, bool BR>
 __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_fwd_big(const uint32_t *in, uint32_t *out, uint32_t npoly,
                                                                         uint32_t ppw)
 {
@@ -349,19 +366,40 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_fwd_big(const
     const uint2 *const tab = reinterpret_cast<const uint2 *>(tabw);
     auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) { big_load_a<BG>(r, in + (size_t)u * N, lane); };
     auto process = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
-        uint32_t lo = lane;   // opaque per unit: scalar base + 32-bit lane offset stores
-        asm volatile("" : "+v"(lo));
-        uint32_t *const dst = out + (size_t)u * N + lo;
-        // every store is a lane-contiguous 256-B run, chunk by chunk (the
-        // stores of chunk c overlap chunk c+1's transpose and arithmetic)
-        big_fwd<BG, 0>(r, buf, tab, h, lane, [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {
-            sfor<32>([&](auto JP) { st_out(dst + BG::boff(C, JP), canon4<P>(v[JP])); });
-        });
+        if constexpr (!BR) {
+            uint32_t lo = lane;   // opaque per unit: scalar base + 32-bit lane offset stores
+            asm volatile("" : "+v"(lo));
+            uint32_t *const dst = out + (size_t)u * N + lo;
+            // every store is a lane-contiguous 256-B run, chunk by chunk (the
+            // stores of chunk c overlap chunk c+1's transpose and arithmetic)
+            big_fwd<BG, 0>(r, buf, tab, h, lane, [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {
+                sfor<32>([&](auto JP) { st_out(dst + BG::boff(C, JP), canon4<P>(v[JP])); });
+            });
+        } else {
+            uint32_t *const dst = out + (size_t)u * N + big_a2_lane<BG>(lane);
+            big_fwd<BG, 0>(r, buf, tab, h, lane, [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {
+                constexpr int c = C;
+                const uint32_t wb = big_wbase(opaque_lane());
+                const Lane<P> LB(opaque_lane());
+                sfor<8>([&](auto Q) {
+                    *reinterpret_cast<uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm)) =
+                        make_uint4(canon4<P>(v[4 * Q + 0]), canon4<P>(v[4 * Q + 1]), canon4<P>(v[4 * Q + 2]),
+                                   canon4<P>(v[4 * Q + 3]));
+                });
+                compiler_fence();
+                sfor<32>([&](auto T) { st_out(dst + BG::aoff(BG::creg(c, T)), buf[big_waddr(wb, T)]); });
+                compiler_fence();   // the next chunk's transpose rewrites buf
+            });
+        }
     };
     big_loop<BG>(npoly, ppw, prologue, load, process);
 }
 
-template <int PS>
+// Inverse, natural-order output.  BR = false: natural-order input (layout
+// B loads); BR = true (poly_invntt_bitrev, input in[t] = X[brv(t)]): layout
+// A'' loads from the words' own positions, each chunk transposed to layout B
+// through the wave's LDS buffer (the forward's transpose) before GS pass 2.
+template <int PS, bool BR>
 __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const uint32_t *in, uint32_t *out, uint32_t npoly,
                                                                         uint32_t ppw)
 {
@@ -376,11 +414,35 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const
     const uint32_t lane = threadIdx.x & 63, h = lane >> 5;
     uint32_t *const buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
     const uint2 *const tab = reinterpret_cast<const uint2 *>(tabw);
-    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) { big_load_b<BG>(r, in + (size_t)u * N, lane); };
+    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
+        if constexpr (!BR) {
+            big_load_b<BG>(r, in + (size_t)u * N, lane);
+        } else {
+            load32n<BG::R>(r, in + (size_t)u * N + big_a2_lane<BG>(lane), [](int j) { return BG::aoff(j); });
+        }
+    };
     auto process = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
         big_inv<BG, 0, false, BG::PL::NINV, BG::PL::C1>(
             r, buf, tab, h, lane,
-            [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) { sfor<32>([&](auto JP) { v[JP] = r[BG::creg(C, JP)]; }); },
+            [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {
+                if constexpr (!BR) {
+                    sfor<32>([&](auto JP) { v[JP] = r[BG::creg(C, JP)]; });
+                } else {
+                    constexpr int c = C;
+                    const uint32_t wb = big_wbase(opaque_lane());
+                    const Lane<typename BG::P> LB(opaque_lane());
+                    sfor<32>([&](auto T) { buf[big_waddr(wb, T)] = r[BG::creg(c, T)]; });
+                    compiler_fence();
+                    sfor<8>([&](auto Q) {
+                        const uint4 x = *reinterpret_cast<const uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm));
+                        v[4 * Q + 0] = x.x;
+                        v[4 * Q + 1] = x.y;
+                        v[4 * Q + 2] = x.z;
+                        v[4 * Q + 3] = x.w;
+                    });
+                    compiler_fence();
+                }
+            },
             out + (size_t)u * N);
     };
     big_loop<BG>(npoly, ppw, prologue, load, process);

@@ -161,11 +161,17 @@ size_t large_ppw(size_t batch, const DevInfo &d)
 // transform kind: forward / inverse with natural or bit-reversed NTT-domain
 // order, or the plain bit-reversal permutation
 enum Xform { FWD, INV, FWD_BR, INV_BR, BITREV };
+static_assert((int)FWD == (int)LAT_FWD && (int)INV == (int)LAT_INV && (int)FWD_BR == (int)LAT_FWD_BR &&
+                  (int)INV_BR == (int)LAT_INV_BR,
+              "switch table order");
+static_assert(LAT_FWD == NTT_OP_FWD && LAT_INV == NTT_OP_INV && LAT_FWD_BR == NTT_OP_FWD_BR &&
+                  LAT_INV_BR == NTT_OP_INV_BR && LAT_MUL == NTT_OP_MUL && LAT_MUL_NTT == NTT_OP_MUL_NTT,
+              "ABI op codes");
 
 template <int PS> struct LXform {
     static int run(Xform k, const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s, const DevInfo &d)
     {
-        if (batch * PSel<PS>::T::N <= (size_t)NTT_LAT_MAX_COEFFS && k != BITREV) {
+        if (k != BITREV && batch <= lat_max_batch(PS, (int)k)) {
             // small batches: one polynomial per workgroup (ntt_lat.hpp)
             const dim3 g((uint32_t)batch), b(LatGeo<PSel<PS>::T::LOGN>::T);
             switch (k) {
@@ -176,29 +182,21 @@ template <int PS> struct LXform {
             default: break;
             }
         } else if constexpr (PS >= LARGE_PS0) {
-            // n = 4096 / 8192: the natural-order transforms; the bit-reversed
-            // orders compose them with the bit-reversal kernel (2 launches)
+            // n = 4096 / 8192: one wave per polynomial (ntt_big.hpp); the
+            // bit-reversed orders are one launch too (an extra LDS transpose per chunk)
             const uint32_t nb = (uint32_t)batch;
             const dim3 gb((uint32_t)(batch < (size_t)d.cus * 64 ? batch : (size_t)d.cus * 64)), bb(512);
-            // one wave per polynomial (ntt_big.hpp)
             using BG = Big<PS>;
             size_t ppw = batch / ((size_t)BG::WAVES * d.cus * 2);
             ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
             const dim3 g((uint32_t)((batch + BG::WAVES * ppw - 1) / (BG::WAVES * ppw))), b(BG::NT);
-            auto fwd = [&](const uint32_t *i, uint32_t *o) { hipLaunchKernelGGL(k_ntt_fwd_big<PS>, g, b, 0, s, i, o, nb, (uint32_t)ppw); };
-            auto inv = [&](const uint32_t *i, uint32_t *o) { hipLaunchKernelGGL(k_ntt_inv_big<PS>, g, b, 0, s, i, o, nb, (uint32_t)ppw); };
+            const uint32_t pw = (uint32_t)ppw;
             switch (k) {
-            case FWD: fwd(in, out); break;
-            case INV: inv(in, out); break;
+            case FWD: hipLaunchKernelGGL((k_ntt_fwd_big<PS, false>), g, b, 0, s, in, out, nb, pw); break;
+            case INV: hipLaunchKernelGGL((k_ntt_inv_big<PS, false>), g, b, 0, s, in, out, nb, pw); break;
+            case FWD_BR: hipLaunchKernelGGL((k_ntt_fwd_big<PS, true>), g, b, 0, s, in, out, nb, pw); break;
+            case INV_BR: hipLaunchKernelGGL((k_ntt_inv_big<PS, true>), g, b, 0, s, in, out, nb, pw); break;
             case BITREV: hipLaunchKernelGGL(k_bitrev_large<PS>, gb, bb, 0, s, in, out, nb); break;
-            case FWD_BR:
-                fwd(in, out);
-                hipLaunchKernelGGL(k_bitrev_large<PS>, gb, bb, 0, s, out, out, nb);
-                break;
-            case INV_BR:
-                hipLaunchKernelGGL(k_bitrev_large<PS>, gb, bb, 0, s, in, out, nb);
-                inv(out, out);
-                break;
             }
         } else {
             const Launch l = launch_for(OP_XFORM, PS, batch, d);
@@ -228,7 +226,7 @@ template <int PS> struct LMul {
                    const DevInfo &d)
     {
         if constexpr (PSel<PS>::T::N <= 4096) {
-            if (batch * PSel<PS>::T::N <= (size_t)NTT_LAT_MUL_MAX_COEFFS) {
+            if (batch <= lat_max_batch(PS, bhat ? LAT_MUL_NTT : LAT_MUL)) {
                 // small batches: one product per workgroup (ntt_lat.hpp)
                 const dim3 g((uint32_t)batch), blk(LatGeo<PSel<PS>::T::LOGN>::T);
                 if (bhat) hipLaunchKernelGGL((k_poly_mul_lat<PS, true>), g, blk, 0, s, a, b, c);
@@ -433,6 +431,15 @@ int ntt_fill_uniform(uint32_t *d_poly, size_t batch, int ps, uint64_t seed, uint
     return finish_launch();
 }
 
+int ntt_small_batch_max(int ps, int op, size_t *max_batch)
+{
+    if (!param_set(ps)) return NTT_ERR_PARAM;
+    if (op < 0 || op >= LAT_NOPS) return NTT_ERR_PARAM;
+    if (!max_batch) return NTT_ERR_NULL;
+    *max_batch = lat_max_batch(ps, op);
+    return NTT_OK;
+}
+
 int ntt_last_hip_error(void) { return t_last_hip; }
 
 int ntt_sync_expiries(uint32_t *count)
@@ -472,7 +479,7 @@ int ntt_build_info(char *buf, size_t len)
     static const char *s =
         "qtesla_ntt gfx950: 1 launch/op, wave-per-poly (n=2048) / half-wave-per-poly (n=1024), 32 coeff/lane, "
         "LDS XOR-swizzled transpose, permlane32 bit-5 stage, Shoup/Harvey lazy CT + signed-Shoup GS butterflies, "
-        "dispatch-ordered unit chunks; small batches (<= " QNTT_STR(NTT_LAT_MAX_COEFFS) " coeffs) one poly per "
+        "dispatch-ordered unit chunks; small batches (per-(n, op) switch, ntt_small_batch_max) one poly per "
         "n/4-thread workgroup; wg=" QNTT_STR(NTT_WG)
         " mul_wg=" QNTT_STR(MUL_WG) " mul_compact=1 ppw<=" QNTT_STR(NTT_PPW_MAX)
         " min_wg/cu=" QNTT_STR(NTT_MIN_WG_PER_CU) "; src=" QNTT_SRC_HASH;

@@ -36,18 +36,38 @@
 
 namespace qntt {
 
-// batches of up to 2^21 coefficients (n = 1024 / 2048 / 4096 / 8192: 2048 /
-// 1024 / 512 / 256 polynomials) take the latency kernels: per launch in a
-// replayed graph they run 2.2 / 2.9 / 4.4 / 8.2 us at batch 1 against 4.5 /
-// 4.9 / 8.7 / 17.1 for the batch kernels, and lose at twice the switch for
-// n = 2048 (11.5 against 10.9 us at 2048 polys) and n = 8192 (36.8 against
-// 33.6 at 1024); the products (n <= 4096) switch at the same size
-// (profiles/r05/lat/)
-#ifndef NTT_LAT_MAX_COEFFS
-#define NTT_LAT_MAX_COEFFS 2097152   // 2^21
-#endif
-#ifndef NTT_LAT_MUL_MAX_COEFFS
-#define NTT_LAT_MUL_MAX_COEFFS 2097152   // 2^21
+// The small-batch switch, one threshold per (parameter set, entry point):
+// batches of up to lat_max_batch(ps, op) polynomials take the latency
+// kernels, larger ones the batch kernels.  Each value is the last batch at
+// which the latency kernel measured faster in round 6's sweep
+// (tools/switch_sweep.py: both paths timed in one process from 64
+// polynomials to the BASELINE batches, doubling, then 8 points per octave
+// around the crossover; profiles/r06/sweep/).  The latency
+// kernels run one polynomial per workgroup with every workgroup resident
+// (n = 2048: ~1 024 at once), so their time steps with each further round of
+// workgroups while the batch kernels' grows smoothly.  Against round 5's
+// single switch of 2^21 coefficients the crossovers lie 1x (the n = 4096
+// products) to 4.5x (the n = 4096 transforms) higher; at the BASELINE batches
+// the latency kernels lose by 1.3-1.5x (p-III forward at 2^20: 4.77 against
+// 3.24 ms), so the headline keeps the batch kernels.
+enum LatOp { LAT_FWD, LAT_INV, LAT_FWD_BR, LAT_INV_BR, LAT_MUL, LAT_MUL_NTT, LAT_NOPS };
+// A/B builds only (tools/switch_sweep.py): NTT_LAT_FORCE 0 sends every batch
+// to the batch kernels, 1 every batch to the latency kernels where they exist
+#ifdef NTT_LAT_FORCE
+constexpr size_t lat_max_batch(int ps, int op)
+{
+    return NTT_LAT_FORCE == 0 ? 0 : (ps == 4 && (op == LAT_MUL || op == LAT_MUL_NTT)) ? 0 : ~(size_t)0;
+}
+#else
+constexpr size_t kLatMaxBatch[5][LAT_NOPS] = {
+    //  fwd   inv  fwd_br inv_br  mul  mul_ntt
+    {3328, 3328, 5632, 6144, 2816, 5120},   // ref   (n = 1024)
+    {3328, 3328, 5632, 6144, 2816, 5120},   // p-I   (n = 1024)
+    {1664, 1664, 3328, 3328, 1280, 1792},   // p-III (n = 2048)
+    {2304, 2560, 2304, 2304, 512, 512},     // n = 4096
+    {768, 768, 768, 768, 0, 0},             // n = 8192 (no latency product)
+};
+constexpr size_t lat_max_batch(int ps, int op) { return kLatMaxBatch[ps][op]; }
 #endif
 
 // full n-point twiddle tables of the n = 4096 / 8192 sets for the latency

@@ -91,6 +91,7 @@ def lib():
         L.ntt_strerror.argtypes = [ctypes.c_int]
         L.ntt_build_info.argtypes = [ctypes.c_char_p, _sz]
         L.ntt_sync_expiries.argtypes = [_u32p]
+        L.ntt_small_batch_max.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_sz)]
         L.ntt_host_ctx_create.argtypes = [ctypes.POINTER(_vp), ctypes.c_int, _sz, ctypes.c_int]
         L.ntt_host_ctx_destroy.argtypes = [_vp]
         for nm in ("poly_ntt_host", "poly_invntt_host"):
@@ -149,6 +150,18 @@ def sync_expiries() -> int:
     device (0 unless a per-polynomial barrier broke; see qtesla_ntt.h)."""
     v = ctypes.c_uint32()
     _check(lib().ntt_sync_expiries(ctypes.byref(v)), "ntt_sync_expiries")
+    return v.value
+
+
+# entry points of the small-batch switch (NTT_OP_* in qtesla_ntt.h)
+SWITCH_OPS = {"fwd": 0, "inv": 1, "fwd_br": 2, "inv_br": 3, "mul": 4, "mul_ntt": 5}
+
+
+def small_batch_max(param_set, op: str) -> int:
+    """Largest batch for which entry point `op` (a SWITCH_OPS key) runs the
+    small-batch kernels, one polynomial per workgroup (0: never)."""
+    v = _sz()
+    _check(lib().ntt_small_batch_max(_ps(param_set), SWITCH_OPS[op], ctypes.byref(v)), "ntt_small_batch_max")
     return v.value
 
 

@@ -169,27 +169,40 @@ def test_pattern_floor_skips_non_transforms_and_missing_library(monkeypatch):
     assert bench.pattern_floor(args, _N8, None, None, None, 10) is None   # n > 2048: no variant
 
 
-def test_latency_threshold_matches_kernels(monkeypatch, tmp_path):
-    """bench.LAT_MAX_COEFFS is the library's small-batch switch
-    (csrc/ntt_lat.hpp); below it a transform line carries no pattern floor
-    (the memory-only variant is the batch kernels')."""
-    import re
+def test_latency_threshold_matches_kernels(ntt, monkeypatch, tmp_path):
+    """bench asks the library which path a batch takes (ntt_small_batch_max,
+    one threshold per (n, op), csrc/ntt_lat.hpp); below the switch a
+    transform line carries no pattern floor (the memory-only variant is the
+    batch kernels')."""
     import types
-    hdr = open(os.path.join(ROOT, "ntt-gpu-qtesla_amd", "csrc", "ntt_lat.hpp")).read()
-    for name in ("NTT_LAT_MAX_COEFFS", "NTT_LAT_MUL_MAX_COEFFS"):
-        m = re.search(rf"#define {name} (\d+)", hdr)
-        assert m and int(m.group(1)) == bench.LAT_MAX_COEFFS, name
-
-    class _N:
-        @staticmethod
-        def param_info(p):
-            return {"n": 1024}
-    lib = tmp_path / "diag.so"
-    lib.write_bytes(b"")
-    monkeypatch.setattr(bench, "DIAG_PATH", str(lib))
+    monkeypatch.setattr(bench, "DIAG_PATH", str(tmp_path / "diag.so"))
+    (tmp_path / "diag.so").write_bytes(b"")
+    m = ntt.small_batch_max("p-I", "fwd")
+    assert m >= 1
+    assert bench.runs_latency_kernels(ntt, "fwd", "p-I", m)
+    assert not bench.runs_latency_kernels(ntt, "fwd", "p-I", m + 1)
+    assert not bench.runs_latency_kernels(ntt, "nussbaumer", "p-III", 1)
     x = types.SimpleNamespace(numel=lambda: 1024)
-    r = bench.pattern_floor(types.SimpleNamespace(op="fwd", param="p-I"), _N, None, x, None, 10)
+    r = bench.pattern_floor(types.SimpleNamespace(op="fwd", param="p-I"), ntt, None, x, None, 10)
     assert "latency kernels" in r["note"]
+
+
+def test_switch_table_in_library(ntt):
+    """ntt_small_batch_max: every (param set, op) answers; the n = 8192 products
+    have no latency kernel (0); bad arguments are rejected without a GPU."""
+    import ctypes
+    for ps in ntt.PARAM_SETS:
+        for op in ntt.SWITCH_OPS:
+            m = ntt.small_batch_max(ps, op)
+            if ntt.param_info(ps)["n"] == 8192 and op.startswith("mul"):
+                assert m == 0
+            else:
+                assert m >= 1, (ps, op)
+    L = ntt.lib()
+    v = ctypes.c_size_t()
+    assert L.ntt_small_batch_max(7, 0, ctypes.byref(v)) == ntt.NTT_ERR_PARAM
+    assert L.ntt_small_batch_max(0, 6, ctypes.byref(v)) == ntt.NTT_ERR_PARAM
+    assert L.ntt_small_batch_max(0, 0, None) == ntt.NTT_ERR_NULL
 
 
 def test_native_latency_reports_instead_of_raising():

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import PARAM_SETS
+from conftest import LARGE_SETS, PARAM_SETS
 
 pytestmark = pytest.mark.gpu
 
@@ -329,28 +329,37 @@ def test_bitrev_copy(ntt, oracle, dev, ps, batch):
     assert np.array_equal(_u32(ntt, t), want)
 
 
-@pytest.mark.parametrize("ps", PARAM_SETS)
-def test_latency_switch_boundary(ntt, oracle, dev, ps):
-    """The last batch the small-batch kernels take (2^21 coefficients) and the
-    first the batch kernels take give the oracle's results for every entry
-    point that switches (csrc/ntt_lat.hpp)."""
-    n = ntt.param_info(ps)["n"]
-    for batch in ((1 << 21) // n, (1 << 21) // n + 1):
+@pytest.mark.parametrize("ps", PARAM_SETS + LARGE_SETS)
+@pytest.mark.parametrize("op", ["fwd", "inv", "fwd_br", "inv_br", "mul", "mul_ntt"])
+def test_latency_switch_boundary(ntt, oracle, dev, ps, op):
+    """The last batch the small-batch kernels take for this entry point
+    (ntt_small_batch_max, one threshold per (n, op), csrc/ntt_lat.hpp) and the
+    first the batch kernels take give the oracle's results."""
+    m = ntt.small_batch_max(ps, op)
+    if m == 0:
+        pytest.skip("no small-batch kernel for this entry point")
+    brv = ntt.tables(ps)["bitrev_tbl"]
+    for batch in (m, m + 1):
         x = oracle.fill_uniform(batch, ps, 0x51DE + batch, 0)
-        y = oracle.fill_uniform(batch, ps, 0x51DF + batch, 0)
-        X = oracle.poly_ntt(x, ps)
-        t = _dev(ntt, x, dev)
-        ntt.poly_ntt(t, ps)
-        assert np.array_equal(_u32(ntt, t), X), batch
-        ntt.poly_invntt(t, ps)
-        assert np.array_equal(_u32(ntt, t), x), batch
-        tx, ty = _dev(ntt, x, dev), _dev(ntt, y, dev)
+        tx = _dev(ntt, x, dev)
         tz = torch.empty_like(tx)
-        ntt.poly_mul(tz, tx, ty, ps)
-        want = oracle.poly_mul(x, y, ps)
-        assert np.array_equal(_u32(ntt, tz), want), batch
-        ntt.poly_mul_ntt(tz, tx, _dev(ntt, oracle.poly_ntt(y, ps), dev), ps)
-        assert np.array_equal(_u32(ntt, tz), want), batch
-        ntt.poly_ntt_bitrev(tz, tx, ps)
-        ntt.poly_invntt_bitrev(tz, tz, ps)
-        assert np.array_equal(_u32(ntt, tz), x), batch
+        if op == "fwd":
+            ntt.poly_ntt(tx, ps)
+            assert np.array_equal(_u32(ntt, tx), oracle.poly_ntt(x, ps)), batch
+        elif op == "inv":
+            ntt.poly_invntt(tx, ps)
+            assert np.array_equal(_u32(ntt, tx), oracle.poly_invntt(x, ps)), batch
+        elif op == "fwd_br":
+            ntt.poly_ntt_bitrev(tz, tx, ps)
+            assert np.array_equal(_u32(ntt, tz), oracle.poly_ntt(x, ps)[:, brv]), batch
+        elif op == "inv_br":
+            ntt.poly_invntt_bitrev(tz, tx, ps)
+            assert np.array_equal(_u32(ntt, tz), oracle.poly_invntt(x[:, brv], ps)), batch
+        else:
+            y = oracle.fill_uniform(batch, ps, 0x51DF + batch, 0)
+            want = oracle.poly_mul(x, y, ps)
+            if op == "mul":
+                ntt.poly_mul(tz, tx, _dev(ntt, y, dev), ps)
+            else:
+                ntt.poly_mul_ntt(tz, tx, _dev(ntt, oracle.poly_ntt(y, ps), dev), ps)
+            assert np.array_equal(_u32(ntt, tz), want), batch

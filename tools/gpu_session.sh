@@ -88,6 +88,17 @@ for step in "$@"; do
         valucost) run valucost 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU --output-format csv -d gpurun_out/valucost -o run -- ./ntt-gpu-qtesla_amd/bin/valu_cost 16384 ;;
         valum_*) n=${step#valum_}; b=$((1073741824 / n)); run valum_$n 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valum_$n -o run -- python3 bench.py --op polymul --param p-III-$n --batch $b --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
         valu_c*) c=${step#valu_c}; run valu_c$c 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valu_c$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
+        # round 6: the small-batch switch per (n, op): latency vs batch kernels
+        # from 64 polynomials to the BASELINE batches (tools/switch_sweep.py)
+        sweep) run sweep 900 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --out gpurun_out/switch_sweep.json ;;
+        sweepfine) run sweepfine 900 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params ref,p-I,p-III,p-III-4096,p-III-8192 --rounds 7 --refine profiles/r06/sweep/switch_sweep_coarse.json --out gpurun_out/switch_sweep_fine.json ;;
+        switchtest) run switchtest 600 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -k "latency_switch or golden" --timeout 120 --timeout-method thread ;;
+        brtest) run brtest 600 python -u -m pytest tests/test_gpu_large.py tests/test_gpu_parity.py -x -q -m gpu -k "bit_reversed or latency_switch or bitrev" --timeout 120 --timeout-method thread ;;
+        abbr) run abbr_4096 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so --param p-III-4096 --batch 524288 --ops fwd,fwdbr,inv,invbr --inplace --rounds 7 &&
+              run abbr_8192 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so --param p-III-8192 --batch 262144 --ops fwd,fwdbr,inv,invbr --inplace --rounds 7 ;;
+        abbr2) run abbr2_4096 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param p-III-4096 --batch 524288 --ops fwd,fwdbr,inv,invbr --inplace --rounds 7 &&
+               run abbr2_8192 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param p-III-8192 --batch 262144 --ops fwd,fwdbr,inv,invbr --inplace --rounds 7 ;;
+        sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
