@@ -303,36 +303,46 @@ def valu_roofline(v, launch_ms: float, hbm: dict) -> dict:
 
 def pattern_floor(args, ntt_amd, torch, x, stream, steps: int):
     """The memory-only variant of the dominant transform kernels: the same
-    grid, work loop, global loads, LDS transposes and stores, no arithmetic
-    (ntt_debug_variant op 0/1 variant 3 of the tools-only diagnostic library,
-    tools/ntt_diag.hip), timed in this process AFTER the timed region on the
-    same buffer (its contents no longer matter), with an event pair around
-    `steps` back-to-back launches on the kernels' stream.  It is the access
-    pattern's own floor: kernel / floor says how much the arithmetic costs
-    the memory stream.  Never part of `value`."""
+    grid, loads, LDS exchanges / transposes and stores, no arithmetic, of the
+    kernel family the line's launches run (tools-only diagnostic library,
+    tools/ntt_diag.hip: ntt_debug_variant op 0/1 variant 3 for the batch
+    kernels, op 5/6 variant 1/5 for the radix-8/16 one-polynomial-per-workgroup
+    kernels), timed in this process AFTER the timed region on the same buffer
+    (its contents no longer matter), with an event pair around `steps`
+    back-to-back launches on the kernels' stream.  It is the access pattern's
+    own floor: kernel / floor says how much the arithmetic costs the memory
+    stream.  Never part of `value`."""
     import ctypes
     if args.op not in ("fwdinv", "fwd", "inv") or ntt_amd.param_info(args.param)["n"] > 2048:
         return None
     if not os.path.exists(DIAG_PATH):
         return {"note": f"{os.path.relpath(DIAG_PATH, ROOT)} not built (make -C ntt-gpu-qtesla_amd tools)"}
-    if runs_latency_kernels(ntt_amd, args.op, args.param, x.numel() // ntt_amd.param_info(args.param)["n"]):
-        return {"note": "small batch: the latency kernels (one polynomial per workgroup, csrc/ntt_lat.hpp) run it; "
-                        "the memory-only variant is the batch kernels' and is not this launch's floor"}
+    npoly = x.numel() // ntt_amd.param_info(args.param)["n"]
+    kinds = {"fwdinv": ["fwd", "inv"], "fwd": ["fwd"], "inv": ["inv"]}[args.op]
+    variants = {}
+    for k in kinds:
+        radix = ntt_amd.small_batch_radix(args.param, k, npoly)
+        if radix == 0:
+            variants[k] = (0 if k == "fwd" else 1, 3, "k_variant<PS, INV, 3> (loads + LDS transpose + stores)")
+        elif radix in (8, 16):
+            variants[k] = (5 if radix == 8 else 6, 1 if k == "fwd" else 5,
+                           f"k_ntt_latr<PS, INV, false, {3 if radix == 8 else 4}, 1> (loads + LDS exchanges + stores)")
+        else:
+            return {"note": "small batch: the radix-4 latency kernels (csrc/ntt_lat.hpp) run it; "
+                            "the diagnostic library has no memory-only variant of them"}
     L = ctypes.CDLL(DIAG_PATH)
     vp = ctypes.c_void_p
     L.ntt_debug_variant.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
     ps = ntt_amd.PARAM_SETS[args.param]
-    npoly = x.numel() // ntt_amd.param_info(args.param)["n"]
-    kinds = {"fwdinv": ["fwd", "inv"], "fwd": ["fwd"], "inv": ["inv"]}[args.op]
     sp = vp(stream.cuda_stream)
     ms = {}
     for k in kinds:
-        op = 0 if k == "fwd" else 1
+        op, var, _ = variants[k]
 
         def run():
-            rc = L.ntt_debug_variant(op, 3, vp(x.data_ptr()), vp(x.data_ptr()), npoly, ps, sp)
+            rc = L.ntt_debug_variant(op, var, vp(x.data_ptr()), vp(x.data_ptr()), npoly, ps, sp)
             if rc != 0:
-                raise RuntimeError(f"ntt_debug_variant({op}, 3) failed: {rc}")
+                raise RuntimeError(f"ntt_debug_variant({op}, {var}) failed: {rc}")
         for _ in range(2):
             run()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -344,7 +354,7 @@ def pattern_floor(args, ntt_amd, torch, x, stream, steps: int):
         torch.cuda.synchronize(x.device)
         ms[k] = e0.elapsed_time(e1) / steps
     return {"ms": ms, "steps": steps,
-            "kernel": "k_variant<PS, INV, 3> (tools/ntt_diag.hip: loads + LDS transpose + stores, no arithmetic)",
+            "kernel": {k: v[2] + ", no arithmetic (tools/ntt_diag.hip)" for k, v in variants.items()},
             "timing": "region events / steps, after the timed region"}
 
 

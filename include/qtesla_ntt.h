@@ -204,8 +204,8 @@ int ntt_sync_expiries(uint32_t *count);
 /* Small-batch switch: writes to *max_batch the largest batch for which
  * entry point `op` (NTT_OP_*) of `param_set` runs the small-batch kernels
  * (one polynomial per workgroup; 0 = never); larger batches
- * run the batch kernels.  Both give identical results; the threshold is the
- * measured crossover of their launch times, one per (n, op).  The reference
+ * run the batch kernels.  All give identical results; the thresholds are the
+ * measured crossovers of their launch times, per (n, op).  The reference
  * has one launch shape for every batch (<<<BATCH, T>>>, NTT.cu:2216). */
 #define NTT_OP_FWD 0     /* poly_ntt, poly_ntt_oop       */
 #define NTT_OP_INV 1     /* poly_invntt, poly_invntt_oop */
@@ -214,6 +214,11 @@ int ntt_sync_expiries(uint32_t *count);
 #define NTT_OP_MUL 4     /* poly_mul                     */
 #define NTT_OP_MUL_NTT 5 /* poly_mul_ntt                 */
 int ntt_small_batch_max(int param_set, int op, size_t *max_batch);
+/* Which kernel family entry point `op` of `param_set` runs at `batch`
+ * polynomials: *radix = 4 / 8 / 16 for the one-polynomial-per-workgroup
+ * kernels with radix-4 / 8 / 16 passes, 0 for the batch
+ * kernels.  Diagnostic; every family gives identical results. */
+int ntt_small_batch_radix(int param_set, int op, size_t batch, int *radix);
 
 /* Library / kernel description for reports, ending in "src=<16 hex>" (a hash
  * of the library sources): writes at most len bytes, returns the length. */

@@ -16,6 +16,7 @@
 #include "ntt_large.hpp"
 #include "ntt_big.hpp"
 #include "ntt_lat.hpp"
+#include "ntt_latr.hpp"
 #include "ntt_internal.h"
 #include "params.hpp"
 #include "pset.hpp"
@@ -169,10 +170,31 @@ static_assert(LAT_FWD == NTT_OP_FWD && LAT_INV == NTT_OP_INV && LAT_FWD_BR == NT
               "ABI op codes");
 
 template <int PS> struct LXform {
+    template <int RB>
+    static void launch_latr(Xform k, const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s)
+    {
+        const dim3 g((uint32_t)batch), b(LatRGeo<PSel<PS>::T::LOGN, RB>::T);
+        switch (k) {
+        case FWD: hipLaunchKernelGGL((k_ntt_latr<PS, false, false, RB>), g, b, 0, s, in, out); break;
+        case INV: hipLaunchKernelGGL((k_ntt_latr<PS, true, false, RB>), g, b, 0, s, in, out); break;
+        case FWD_BR: hipLaunchKernelGGL((k_ntt_latr<PS, false, true, RB>), g, b, 0, s, in, out); break;
+        case INV_BR: hipLaunchKernelGGL((k_ntt_latr<PS, true, true, RB>), g, b, 0, s, in, out); break;
+        default: break;
+        }
+    }
     static int run(Xform k, const uint32_t *in, uint32_t *out, size_t batch, hipStream_t s, const DevInfo &d)
     {
-        if (k != BITREV && batch <= lat_max_batch(PS, (int)k)) {
-            // small batches: one polynomial per workgroup (ntt_lat.hpp)
+#ifdef NTT_LATR_FORCE
+        // A/B builds only: every transform on the radix-2^NTT_LATR_FORCE
+        // workgroup-per-polynomial kernels (ntt_latr.hpp)
+        if (k != BITREV) {
+            launch_latr<NTT_LATR_FORCE>(k, in, out, batch, s);
+            return finish_launch();
+        }
+#endif
+        const int rb = k == BITREV ? 0 : lat_radix(PS, (int)k, batch);
+        if (rb == 2) {
+            // small batches: radix-4 passes, one polynomial per n/4-thread workgroup (ntt_lat.hpp)
             const dim3 g((uint32_t)batch), b(LatGeo<PSel<PS>::T::LOGN>::T);
             switch (k) {
             case FWD: hipLaunchKernelGGL((k_ntt_lat<PS, false, false>), g, b, 0, s, in, out); break;
@@ -181,6 +203,10 @@ template <int PS> struct LXform {
             case INV_BR: hipLaunchKernelGGL((k_ntt_lat<PS, true, true>), g, b, 0, s, in, out); break;
             default: break;
             }
+        } else if (rb == 3) {
+            launch_latr<3>(k, in, out, batch, s);   // radix-8 passes, n/8 threads (ntt_latr.hpp)
+        } else if (rb == 4) {
+            launch_latr<4>(k, in, out, batch, s);   // radix-16 passes, n/16 threads
         } else if constexpr (PS >= LARGE_PS0) {
             // n = 4096 / 8192: one wave per polynomial (ntt_big.hpp); the
             // bit-reversed orders are one launch too (an extra LDS transpose per chunk)
@@ -437,6 +463,16 @@ int ntt_small_batch_max(int ps, int op, size_t *max_batch)
     if (op < 0 || op >= LAT_NOPS) return NTT_ERR_PARAM;
     if (!max_batch) return NTT_ERR_NULL;
     *max_batch = lat_max_batch(ps, op);
+    return NTT_OK;
+}
+
+int ntt_small_batch_radix(int ps, int op, size_t batch, int *radix)
+{
+    if (!param_set(ps)) return NTT_ERR_PARAM;
+    if (op < 0 || op >= LAT_NOPS) return NTT_ERR_PARAM;
+    if (!radix) return NTT_ERR_NULL;
+    const int rb = lat_radix(ps, op, batch);
+    *radix = rb ? 1 << rb : 0;
     return NTT_OK;
 }
 

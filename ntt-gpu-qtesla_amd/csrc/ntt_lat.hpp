@@ -36,39 +36,60 @@
 
 namespace qntt {
 
-// The small-batch switch, one threshold per (parameter set, entry point):
-// batches of up to lat_max_batch(ps, op) polynomials take the latency
-// kernels, larger ones the batch kernels.  Each value is the last batch at
-// which the latency kernel measured faster in round 6's sweep
-// (tools/switch_sweep.py: both paths timed in one process from 64
-// polynomials to the BASELINE batches, doubling, then 8 points per octave
-// around the crossover; profiles/r06/sweep/).  The latency
-// kernels run one polynomial per workgroup with every workgroup resident
-// (n = 2048: ~1 024 at once), so their time steps with each further round of
-// workgroups while the batch kernels' grows smoothly.  Against round 5's
-// single switch of 2^21 coefficients the crossovers lie 1x (the n = 4096
-// products) to 4.5x (the n = 4096 transforms) higher; at the BASELINE batches
-// the latency kernels lose by 1.3-1.5x (p-III forward at 2^20: 4.77 against
-// 3.24 ms), so the headline keeps the batch kernels.
+// The small-batch switch (entry points of include/qtesla_ntt.h NTT_OP_*):
+// up to two tiers of one-polynomial-per-workgroup kernels per (parameter
+// set, entry point) before the batch kernels take over -- tier 0 for batches
+// up to max0 with radix rb0, tier 1 up to max1 with radix rb1 (rb = 2: the
+// radix-4 kernels of this file, 3 / 4: the radix-8 / radix-16 ones of
+// ntt_latr.hpp; the products have radix-4 kernels only).  Round 6 set them
+// from sweeps that time every family against the batch kernels in one
+// process from 64 polynomials to the BASELINE batches (tools/switch_sweep.py,
+// profiles/r06/sweep/, profiles/r06/latr/) and the per-launch latency of
+// batches 1-256 (tools/latency.py, profiles/r06/latr/latsmall_*.log): each max
+// is the last measured batch at which that family beat the batch kernels.
+// The one-polynomial-per-workgroup kernels keep the memory system's fast
+// regime (short-lived workgroups) but pay their twiddles per
+// polynomial; at the BASELINE batches the batch kernels stay ahead (p-III
+// forward at 2^20: 3.23 ms against 3.38 / 3.50 ms radix-8 / 16, 4.77 radix-4),
+// except at n = 1024 where radix-16 (one wave per polynomial) runs level.
 enum LatOp { LAT_FWD, LAT_INV, LAT_FWD_BR, LAT_INV_BR, LAT_MUL, LAT_MUL_NTT, LAT_NOPS };
+struct LatTier {
+    int rb0;
+    size_t max0;
+    int rb1;
+    size_t max1;
+};
 // A/B builds only (tools/switch_sweep.py): NTT_LAT_FORCE 0 sends every batch
-// to the batch kernels, 1 every batch to the latency kernels where they exist
+// to the batch kernels, 1 every batch to the radix-4 kernels where they exist
 #ifdef NTT_LAT_FORCE
-constexpr size_t lat_max_batch(int ps, int op)
+constexpr LatTier lat_tier(int ps, int op)
 {
-    return NTT_LAT_FORCE == 0 ? 0 : (ps == 4 && (op == LAT_MUL || op == LAT_MUL_NTT)) ? 0 : ~(size_t)0;
+    return NTT_LAT_FORCE == 0 || (ps == 4 && (op == LAT_MUL || op == LAT_MUL_NTT)) ? LatTier{2, 0, 2, 0}
+                                                                                    : LatTier{2, ~(size_t)0, 2, 0};
 }
 #else
-constexpr size_t kLatMaxBatch[5][LAT_NOPS] = {
-    //  fwd   inv  fwd_br inv_br  mul  mul_ntt
-    {3328, 3328, 5632, 6144, 2816, 5120},   // ref   (n = 1024)
-    {3328, 3328, 5632, 6144, 2816, 5120},   // p-I   (n = 1024)
-    {1664, 1664, 3328, 3328, 1280, 1792},   // p-III (n = 2048)
-    {2304, 2560, 2304, 2304, 512, 512},     // n = 4096
-    {768, 768, 768, 768, 0, 0},             // n = 8192 (no latency product)
+constexpr LatTier kLatTier[5][LAT_NOPS] = {
+    // fwd                     inv                        fwd_br                  inv_br                   mul              mul_ntt
+    {{2, 1024, 4, 262144}, {2, 1024, 4, 262144}, {2, 1024, 3, 4096}, {2, 1024, 3, 32768}, {2, 2816, 0, 0}, {2, 5120, 0, 0}},   // ref
+    {{2, 1024, 4, 262144}, {2, 1024, 4, 262144}, {2, 1024, 3, 4096}, {2, 1024, 3, 32768}, {2, 2816, 0, 0}, {2, 5120, 0, 0}},   // p-I
+    {{3, 65536, 0, 0}, {3, 32768, 0, 0}, {3, 2048, 0, 0}, {3, 2048, 0, 0}, {2, 1280, 0, 0}, {2, 1792, 0, 0}},                  // p-III
+    {{4, 16384, 0, 0}, {3, 32768, 0, 0}, {3, 2048, 0, 0}, {3, 16384, 0, 0}, {2, 512, 0, 0}, {2, 512, 0, 0}},                   // n = 4096
+    {{4, 32768, 0, 0}, {4, 32768, 0, 0}, {4, 1024, 0, 0}, {3, 16384, 0, 0}, {2, 0, 0, 0}, {2, 0, 0, 0}},                       // n = 8192
 };
-constexpr size_t lat_max_batch(int ps, int op) { return kLatMaxBatch[ps][op]; }
+constexpr LatTier lat_tier(int ps, int op) { return kLatTier[ps][op]; }
 #endif
+// the largest batch any small-batch tier takes (0: none)
+constexpr size_t lat_max_batch(int ps, int op)
+{
+    const LatTier t = lat_tier(ps, op);
+    return t.max1 > t.max0 ? t.max1 : t.max0;
+}
+// radix bits of the small-batch kernel for `batch` (0: the batch kernels)
+constexpr int lat_radix(int ps, int op, size_t batch)
+{
+    const LatTier t = lat_tier(ps, op);
+    return batch <= t.max0 ? t.rb0 : batch <= t.max1 ? t.rb1 : 0;
+}
 
 // full n-point twiddle tables of the n = 4096 / 8192 sets for the latency
 // kernels (the batch kernels there read per-chunk images), [fwd / inv][k],

@@ -92,6 +92,7 @@ def lib():
         L.ntt_build_info.argtypes = [ctypes.c_char_p, _sz]
         L.ntt_sync_expiries.argtypes = [_u32p]
         L.ntt_small_batch_max.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_sz)]
+        L.ntt_small_batch_radix.argtypes = [ctypes.c_int, ctypes.c_int, _sz, ctypes.POINTER(ctypes.c_int)]
         L.ntt_host_ctx_create.argtypes = [ctypes.POINTER(_vp), ctypes.c_int, _sz, ctypes.c_int]
         L.ntt_host_ctx_destroy.argtypes = [_vp]
         for nm in ("poly_ntt_host", "poly_invntt_host"):
@@ -162,6 +163,14 @@ def small_batch_max(param_set, op: str) -> int:
     small-batch kernels, one polynomial per workgroup (0: never)."""
     v = _sz()
     _check(lib().ntt_small_batch_max(_ps(param_set), SWITCH_OPS[op], ctypes.byref(v)), "ntt_small_batch_max")
+    return v.value
+
+
+def small_batch_radix(param_set, op: str, batch: int) -> int:
+    """Radix of the one-polynomial-per-workgroup kernel entry point `op`
+    runs at `batch` polynomials (4 / 8 / 16), 0 for the batch kernels."""
+    v = ctypes.c_int()
+    _check(lib().ntt_small_batch_radix(_ps(param_set), SWITCH_OPS[op], batch, ctypes.byref(v)), "ntt_small_batch_radix")
     return v.value
 
 

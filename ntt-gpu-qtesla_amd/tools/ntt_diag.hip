@@ -14,6 +14,12 @@
 //   op 4       the round-3 workgroup-per-polynomial n = 2048 transforms
 //              (ntt_wg.hpp): variant 0 / 1 forward persistent /
 //              one polynomial per workgroup, 2 / 3 the same inverses
+//   op 5 / 6   the radix-8 / radix-16 workgroup-per-polynomial transforms
+//              (csrc/ntt_latr.hpp, n <= 2048, one polynomial per workgroup):
+//              variants 0-3 forward, 4-7 inverse: full, memory only (loads, LDS
+//              exchanges and barriers, stores), arithmetic + twiddle loads +
+//              LDS only (no global data traffic), memory only plus the twiddle
+//              loads
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -23,6 +29,7 @@
 #include "../csrc/dev_tables.hpp"
 #include "../csrc/ntt_device.hpp"
 #include "ntt_wg.hpp"
+#include "../csrc/ntt_latr.hpp"
 
 namespace qntt {
 namespace {
@@ -196,6 +203,35 @@ extern "C" int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uin
         default: return NTT_ERR_PARAM;
         }
         return hipGetLastError() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    }
+    if (op == 5 || op == 6) {   // one polynomial per workgroup: the grid is the batch
+        const dim3 g((uint32_t)batch);
+        auto run = [&](auto PSI, auto RBI) {
+            constexpr int PS = decltype(PSI)::value, RB = decltype(RBI)::value;
+            const dim3 b(LatRGeo<PSel<PS>::T::LOGN, RB>::T);
+            switch (variant) {
+            case 0: hipLaunchKernelGGL((k_ntt_latr<PS, false, false, RB, 0>), g, b, 0, s, d_in, d_out); break;
+            case 1: hipLaunchKernelGGL((k_ntt_latr<PS, false, false, RB, 1>), g, b, 0, s, d_in, d_out); break;
+            case 2: hipLaunchKernelGGL((k_ntt_latr<PS, false, false, RB, 2>), g, b, 0, s, d_in, d_out); break;
+            case 3: hipLaunchKernelGGL((k_ntt_latr<PS, false, false, RB, 3>), g, b, 0, s, d_in, d_out); break;
+            case 4: hipLaunchKernelGGL((k_ntt_latr<PS, true, false, RB, 0>), g, b, 0, s, d_in, d_out); break;
+            case 5: hipLaunchKernelGGL((k_ntt_latr<PS, true, false, RB, 1>), g, b, 0, s, d_in, d_out); break;
+            case 6: hipLaunchKernelGGL((k_ntt_latr<PS, true, false, RB, 2>), g, b, 0, s, d_in, d_out); break;
+            case 7: hipLaunchKernelGGL((k_ntt_latr<PS, true, false, RB, 3>), g, b, 0, s, d_in, d_out); break;
+            default: return (int)NTT_ERR_PARAM;
+            }
+            return hipGetLastError() == hipSuccess ? (int)NTT_OK : (int)NTT_ERR_HIP;
+        };
+        using R3 = std::integral_constant<int, 3>;
+        using R4 = std::integral_constant<int, 4>;
+        switch (ps * 2 + (op == 6)) {
+        case 0: return run(std::integral_constant<int, 0>{}, R3{});
+        case 1: return run(std::integral_constant<int, 0>{}, R4{});
+        case 2: return run(std::integral_constant<int, 1>{}, R3{});
+        case 3: return run(std::integral_constant<int, 1>{}, R4{});
+        case 4: return run(std::integral_constant<int, 2>{}, R3{});
+        default: return run(std::integral_constant<int, 2>{}, R4{});
+        }
     }
     if (op != 0 && op != 1 && op != 3) return NTT_ERR_PARAM;
     switch (ps) {

@@ -170,10 +170,10 @@ def test_pattern_floor_skips_non_transforms_and_missing_library(monkeypatch):
 
 
 def test_latency_threshold_matches_kernels(ntt, monkeypatch, tmp_path):
-    """bench asks the library which path a batch takes (ntt_small_batch_max,
-    one threshold per (n, op), csrc/ntt_lat.hpp); below the switch a
-    transform line carries no pattern floor (the memory-only variant is the
-    batch kernels')."""
+    """bench asks the library which path a batch takes (ntt_small_batch_max /
+    ntt_small_batch_radix, csrc/ntt_lat.hpp); on the radix-4 small-batch
+    kernels a transform line carries no pattern floor (the diagnostic library
+    has no memory-only variant of them)."""
     import types
     monkeypatch.setattr(bench, "DIAG_PATH", str(tmp_path / "diag.so"))
     (tmp_path / "diag.so").write_bytes(b"")
@@ -182,27 +182,38 @@ def test_latency_threshold_matches_kernels(ntt, monkeypatch, tmp_path):
     assert bench.runs_latency_kernels(ntt, "fwd", "p-I", m)
     assert not bench.runs_latency_kernels(ntt, "fwd", "p-I", m + 1)
     assert not bench.runs_latency_kernels(ntt, "nussbaumer", "p-III", 1)
+    assert ntt.small_batch_radix("p-I", "fwd", 1) == 4
     x = types.SimpleNamespace(numel=lambda: 1024)
     r = bench.pattern_floor(types.SimpleNamespace(op="fwd", param="p-I"), ntt, None, x, None, 10)
-    assert "latency kernels" in r["note"]
+    assert "radix-4" in r["note"]
 
 
 def test_switch_table_in_library(ntt):
-    """ntt_small_batch_max: every (param set, op) answers; the n = 8192 products
-    have no latency kernel (0); bad arguments are rejected without a GPU."""
+    """ntt_small_batch_max / ntt_small_batch_radix: every (param set, op)
+    answers; the tiers only grow the radix-4 -> 8 -> 16 order below the max
+    and the batch kernels (0) run above it; the n = 8192 products have no
+    small-batch kernel; bad arguments are rejected without a GPU."""
     import ctypes
     for ps in ntt.PARAM_SETS:
         for op in ntt.SWITCH_OPS:
             m = ntt.small_batch_max(ps, op)
             if ntt.param_info(ps)["n"] == 8192 and op.startswith("mul"):
                 assert m == 0
-            else:
-                assert m >= 1, (ps, op)
+                continue
+            assert m >= 1, (ps, op)
+            assert ntt.small_batch_radix(ps, op, m) in (4, 8, 16)
+            assert ntt.small_batch_radix(ps, op, m + 1) == 0
+            assert ntt.small_batch_radix(ps, op, 1) in (4, 8, 16)
+            if op.startswith("mul"):
+                assert ntt.small_batch_radix(ps, op, m) == 4   # the products: radix-4 kernels only
     L = ntt.lib()
     v = ctypes.c_size_t()
+    r = ctypes.c_int()
     assert L.ntt_small_batch_max(7, 0, ctypes.byref(v)) == ntt.NTT_ERR_PARAM
     assert L.ntt_small_batch_max(0, 6, ctypes.byref(v)) == ntt.NTT_ERR_PARAM
     assert L.ntt_small_batch_max(0, 0, None) == ntt.NTT_ERR_NULL
+    assert L.ntt_small_batch_radix(0, 6, 1, ctypes.byref(r)) == ntt.NTT_ERR_PARAM
+    assert L.ntt_small_batch_radix(0, 0, 1, None) == ntt.NTT_ERR_NULL
 
 
 def test_native_latency_reports_instead_of_raising():

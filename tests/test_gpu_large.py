@@ -189,10 +189,10 @@ def test_large_bit_reversed_orders(ntt, oracle, dev, ps):
     log2 n = 12 / 13 bits, in and out of place; poly_ntt_bitrev =
     bitrev(poly_ntt); poly_invntt_bitrev on bit-reversed input = the CT
     inverse (oracle_poly_invntt_ct) = poly_invntt."""
-    # the last batch: past the small-batch switch of both bit-reversed entry
-    # points (the one-launch batch kernels, ntt_big.hpp BR = true), odd
-    past = max(ntt.small_batch_max(ps, "fwd_br"), ntt.small_batch_max(ps, "inv_br")) + 1
-    for batch in (1, 3, 130, past | 1):
+    # all on the small-batch kernels; both sides of every switch point of the
+    # bit-reversed entry points (the one-launch batch kernels, ntt_big.hpp
+    # BR = true, above it) are test_gpu_parity.py::test_latency_switch_boundary's
+    for batch in (1, 3, 130, 600):
         x = oracle.fill_uniform(batch, ps, 0xB17 + batch, 0)
         tx = _dev(ntt, x, dev)
         ty = torch.empty_like(tx)

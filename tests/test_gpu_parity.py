@@ -329,37 +329,71 @@ def test_bitrev_copy(ntt, oracle, dev, ps, batch):
     assert np.array_equal(_u32(ntt, t), want)
 
 
+def _switch_points(ntt, ps, op):
+    """Every batch at which entry point `op` changes kernel family
+    (ntt_small_batch_radix: radix-4 / 8 / 16 one-polynomial-per-workgroup
+    tiers, then the batch kernels), found by bisection: the last batch of each
+    tier and the first of the next."""
+    m = ntt.small_batch_max(ps, op)
+    pts = []
+    lo = 1
+    while lo <= m:
+        r = ntt.small_batch_radix(ps, op, lo)
+        a, b = lo, m + 1          # radix(a) == r, radix(b) != r
+        while b - a > 1:
+            mid = (a + b) // 2
+            if ntt.small_batch_radix(ps, op, mid) == r:
+                a = mid
+            else:
+                b = mid
+        pts += [a, b]
+        lo = b
+    return sorted(set(pts))
+
+
 @pytest.mark.parametrize("ps", PARAM_SETS + LARGE_SETS)
 @pytest.mark.parametrize("op", ["fwd", "inv", "fwd_br", "inv_br", "mul", "mul_ntt"])
 def test_latency_switch_boundary(ntt, oracle, dev, ps, op):
-    """The last batch the small-batch kernels take for this entry point
-    (ntt_small_batch_max, one threshold per (n, op), csrc/ntt_lat.hpp) and the
-    first the batch kernels take give the oracle's results."""
-    m = ntt.small_batch_max(ps, op)
-    if m == 0:
+    """On both sides of every switch point of this entry point (the tiers of
+    csrc/ntt_lat.hpp: radix-4 / 8 / 16 one-polynomial-per-workgroup kernels,
+    then the batch kernels) the results equal the oracle's.  Inputs come from
+    the device generator; 40 sampled polynomials of each launch (first, last,
+    random) are regenerated on the host and checked."""
+    if ntt.small_batch_max(ps, op) == 0:
         pytest.skip("no small-batch kernel for this entry point")
+    n = ntt.param_info(ps)["n"]
     brv = ntt.tables(ps)["bitrev_tbl"]
-    for batch in (m, m + 1):
-        x = oracle.fill_uniform(batch, ps, 0x51DE + batch, 0)
-        tx = _dev(ntt, x, dev)
+    for batch in _switch_points(ntt, ps, op):
+        rows = sorted({0, 1, batch // 2, batch - 2, batch - 1} |
+                      set(np.random.default_rng(batch).integers(0, batch, 35).tolist()))
+        rows = [r for r in rows if 0 <= r < batch]
+        ri = torch.tensor(rows, device=dev)
+        seed = 0x51DE + batch
+        tx = torch.empty(batch * n, dtype=torch.int32, device=dev)
+        ntt.fill_uniform(tx, ps, seed)
+        xs = np.concatenate([oracle.fill_uniform(1, ps, seed, r) for r in rows])
         tz = torch.empty_like(tx)
+        got = lambda t: _u32(ntt, t.view(batch, n)[ri])   # noqa: E731
         if op == "fwd":
             ntt.poly_ntt(tx, ps)
-            assert np.array_equal(_u32(ntt, tx), oracle.poly_ntt(x, ps)), batch
+            assert np.array_equal(got(tx), oracle.poly_ntt(xs, ps)), batch
         elif op == "inv":
             ntt.poly_invntt(tx, ps)
-            assert np.array_equal(_u32(ntt, tx), oracle.poly_invntt(x, ps)), batch
+            assert np.array_equal(got(tx), oracle.poly_invntt(xs, ps)), batch
         elif op == "fwd_br":
             ntt.poly_ntt_bitrev(tz, tx, ps)
-            assert np.array_equal(_u32(ntt, tz), oracle.poly_ntt(x, ps)[:, brv]), batch
+            assert np.array_equal(got(tz), oracle.poly_ntt(xs, ps)[:, brv]), batch
         elif op == "inv_br":
             ntt.poly_invntt_bitrev(tz, tx, ps)
-            assert np.array_equal(_u32(ntt, tz), oracle.poly_invntt(x[:, brv], ps)), batch
+            assert np.array_equal(got(tz), oracle.poly_invntt(xs[:, brv], ps)), batch
         else:
-            y = oracle.fill_uniform(batch, ps, 0x51DF + batch, 0)
-            want = oracle.poly_mul(x, y, ps)
+            ty = torch.empty_like(tx)
+            ntt.fill_uniform(ty, ps, seed + 1)
+            ys = np.concatenate([oracle.fill_uniform(1, ps, seed + 1, r) for r in rows])
+            want = oracle.poly_mul(xs, ys, ps)
             if op == "mul":
-                ntt.poly_mul(tz, tx, _dev(ntt, y, dev), ps)
+                ntt.poly_mul(tz, tx, ty, ps)
             else:
-                ntt.poly_mul_ntt(tz, tx, _dev(ntt, oracle.poly_ntt(y, ps), dev), ps)
-            assert np.array_equal(_u32(ntt, tz), want), batch
+                ntt.poly_ntt(ty, ps)   # b-hat; verified by the "fwd" case
+                ntt.poly_mul_ntt(tz, tx, ty, ps)
+            assert np.array_equal(got(tz), want), batch

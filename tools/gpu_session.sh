@@ -98,6 +98,16 @@ for step in "$@"; do
               run abbr_8192 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so --param p-III-8192 --batch 262144 --ops fwd,fwdbr,inv,invbr --inplace --rounds 7 ;;
         abbr2) run abbr2_4096 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param p-III-4096 --batch 524288 --ops fwd,fwdbr,inv,invbr --inplace --rounds 7 &&
                run abbr2_8192 300 python tools/ab.py ntt-gpu-qtesla_amd/lib/ab/*.so --param p-III-8192 --batch 262144 --ops fwd,fwdbr,inv,invbr --inplace --rounds 7 ;;
+        ab8) L="ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so ntt-gpu-qtesla_amd/lib/ab8/*.so";
+             run ab8_p3 300 python tools/ab.py $L --param p-III --batch 1048576 --ops fwd,inv,fwdbr,invbr --rounds 7 &&
+             run ab8_p1 300 python tools/ab.py $L --param p-I --batch 1048576 --ops fwd,inv --rounds 7 &&
+             run ab8_4096 300 python tools/ab.py $L --param p-III-4096 --batch 524288 --ops fwd,inv --rounds 7 &&
+             run ab8_8192 300 python tools/ab.py $L --param p-III-8192 --batch 262144 --ops fwd,inv --rounds 7 ;;
+        sweep8) run sweep8 900 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so ntt-gpu-qtesla_amd/lib/ab8/lat8.so ntt-gpu-qtesla_amd/lib/ab8/lat16.so --ops fwd,inv,fwdbr,invbr --rounds 5 --out gpurun_out/switch_sweep_latr.json ;;
+        floor8) run floor8_p3 300 python tools/latr_floor.py --param p-III &&
+                run floor8_p1 300 python tools/latr_floor.py --param p-I ;;
+        latsmall) for f in sweep/b_lat ab8/lat8 ab8/lat16; do b=$(basename $f);
+                      run latsmall_$b 300 python tools/latency.py --lib ntt-gpu-qtesla_amd/lib/$f.so --batches 1,8,64,256 --params p-I,p-III,p-III-4096,p-III-8192 --rounds 5 || exit 1; done ;;
         sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac

@@ -14,7 +14,7 @@ point is one HIP event pair around K back-to-back launches (K sized so the
 region is >= ~2 ms, at most 200), median over rounds.  Outputs are checked
 equal between the builds.
 
-    python tools/switch_sweep.py BATCH.so LAT.so [--params p-I,p-III] [--ops fwd,inv,...]
+    python tools/switch_sweep.py BATCH.so SMALL.so [SMALL2.so ...] [--params p-I,p-III] [--ops fwd,inv,...]
 """
 import argparse
 import ctypes
@@ -35,7 +35,7 @@ MAX_BATCH = {1024: 1 << 20, 2048: 1 << 20, 4096: 1 << 19, 8192: 1 << 18}
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("batch_lib")
-    ap.add_argument("lat_lib")
+    ap.add_argument("lat_lib", nargs="+", help="one or more builds whose small-batch path to compare (tag = file name)")
     ap.add_argument("--params", default="p-I,p-III,p-III-4096,p-III-8192")
     ap.add_argument("--ops", default="fwd,inv,fwdbr,invbr,mul,mulntt")
     ap.add_argument("--rounds", type=int, default=5)
@@ -50,7 +50,7 @@ def main():
     import ntt_amd
     vp, sz = ctypes.c_void_p, ctypes.c_size_t
     libs = {}
-    for tag, path in (("batch", args.batch_lib), ("lat", args.lat_lib)):
+    for tag, path in [("batch", args.batch_lib)] + [(os.path.basename(p)[:-3], p) for p in args.lat_lib]:
         L = ctypes.CDLL(os.path.abspath(path))
         for nm in ("poly_ntt_oop", "poly_invntt_oop", "poly_ntt_bitrev", "poly_invntt_bitrev"):
             getattr(L, nm).argtypes = [vp, vp, sz, ctypes.c_int, vp]
@@ -108,7 +108,7 @@ def main():
                     launch(L)
                     torch.cuda.synchronize()
                     sig[tag] = z[: b * n: 4099].clone()
-                same = bool(torch.equal(sig["batch"], sig["lat"]))
+                same = all(bool(torch.equal(sig["batch"], v)) for v in sig.values())
                 # one probe launch of the batch build sizes K
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
@@ -130,24 +130,33 @@ def main():
                 r["k"] = k
                 r["same"] = same
                 res.setdefault(param, {}).setdefault(op, {})[b] = r
-                print(f"[{time.time() - t_start:6.1f}s] {param} {op} b={b}: batch {r['batch']} us, "
-                      f"lat {r['lat']} us, same={same}", flush=True)
+                print(f"[{time.time() - t_start:6.1f}s] {param} {op} b={b}: " +
+                      ", ".join(f"{tag} {r[tag]} us" for tag in libs) + f", same={same}", flush=True)
         del x, y, z
         torch.cuda.empty_cache()
-    # crossover: the largest batch up to which the latency kernel wins at
-    # every measured point (the switch is one threshold per (n, op))
+    # per (n, op): the fastest build at every batch, and for each small-batch
+    # build the largest batch up to which it beats the batch kernels at every
+    # measured point (the switch is one threshold per (n, op))
     summary = {}
     for param, ops in res.items():
         for op, pts in ops.items():
-            last_win = 0
-            for b in sorted(pts):
-                if pts[b]["lat"] < pts[b]["batch"]:
-                    last_win = b
-                else:
-                    break
-            summary[f"{param}:{op}"] = {"lat_wins_through": last_win,
-                                        "lat_wins_at": [b for b in sorted(pts) if pts[b]["lat"] < pts[b]["batch"]]}
-    out = {"rounds": args.rounds, "libs": {"batch": args.batch_lib, "lat": args.lat_lib},
+            ent = {"fastest": {str(b): min((t for t in libs), key=lambda t: pts[b][t]) for b in sorted(pts)}}
+            for tag in libs:
+                if tag == "batch":
+                    continue
+                last_win = 0
+                for b in sorted(pts):
+                    if pts[b][tag] < pts[b]["batch"]:
+                        last_win = b
+                    else:
+                        break
+                ent[tag] = {"wins_through": last_win,
+                            "wins_at": [b for b in sorted(pts) if pts[b][tag] < pts[b]["batch"]]}
+            # round 5/6 field name for the radix-4 build (b_lat)
+            first = next(t for t in libs if t != "batch")
+            ent["lat_wins_through"] = ent[first]["wins_through"]
+            summary[f"{param}:{op}"] = ent
+    out = {"rounds": args.rounds, "libs": {"batch": args.batch_lib, "small": args.lat_lib},
            "results": {p: {o: {str(b): v for b, v in pts.items()} for o, pts in ops.items()} for p, ops in res.items()},
            "summary": summary}
     txt = json.dumps(out, indent=1)
