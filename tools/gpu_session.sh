@@ -12,7 +12,23 @@ run() {
     case $rc in 124|137|134|139|135|136) echo "fatal rc=$rc in $name, stopping"; exit $rc;; esac
     return 0
 }
+# named step groups: `final` (one round's full measurement of the tree's
+# build: GPU tests, smoke, every bench line with its CPU baselines, rocprofv3
+# kernel stats, FETCH / WRITE PMC and VALU counters of every workload, config
+# 5's SQ counters; tools/archive_final.sh + tools/valu_summary.py turn its
+# gpurun_out/ into profiles/<round>/final/ and profiles/pmc_summary.json) and
+# `verify` (the default bench and the VALU-bound lines on the committed summary)
+steps=()
 for step in "$@"; do
+    case $step in
+        final) steps+=(pytest smoke bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 benchl_4096 benchl_8192 benchm_4096 benchm_8192
+                       prof_c2 prof_c3 prof_c4 prof_c5 profl_4096 profl_8192 profm_4096 profm_8192
+                       pmc_c2 pmc_c3 pmc_c4 pmc_c5 pmcl_4096 pmcl_8192 pmcm_4096 pmcm_8192 valu_c4 valu_c5 valum_4096 valum_8192 sq_c5 sqb_c5) ;;
+        verify) steps+=(bench bench_c4 bench_c5 benchm_4096 benchm_8192) ;;
+        *) steps+=("$step") ;;
+    esac
+done
+for step in "${steps[@]}"; do
     case $step in
         valu)   run valu 60 ./ntt-gpu-qtesla_amd/bin/valu_rates ;;
         smoke)  run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -108,6 +124,10 @@ for step in "$@"; do
                 run floor8_p1 300 python tools/latr_floor.py --param p-I ;;
         latsmall) for f in sweep/b_lat ab8/lat8 ab8/lat16; do b=$(basename $f);
                       run latsmall_$b 300 python tools/latency.py --lib ntt-gpu-qtesla_amd/lib/$f.so --batches 1,8,64,256 --params p-I,p-III,p-III-4096,p-III-8192 --rounds 5 || exit 1; done ;;
+        ab9) L="ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so ntt-gpu-qtesla_amd/lib/ab9/*.so";
+             run ab9_chk 300 python tools/ab.py $L --param p-III --batch 65536 --ops fwd,inv,fwdbr,invbr --rounds 2 &&
+             run ab9_p3 300 python tools/ab.py $L --param p-III --batch 1048576 --ops fwd,inv --inplace --rounds 9 &&
+             run ab9_p1 300 python tools/ab.py $L --param p-I --batch 1048576 --ops fwd,inv --inplace --rounds 9 ;;
         sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
