@@ -294,9 +294,11 @@ def valu_roofline(v, launch_ms: float, hbm: dict) -> dict:
     cyc = v["valu_simd_cycles_per_launch"]
     achieved = cyc / (launch_ms * 1e-3) / 1e9
     peak = SIMDS_PER_CU * v["cus"] * PEAK_CLOCK_GHZ
+    held = v.get("valu_busy_at_pmc_clock")
     return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G SIMD-cycles/s", "frac": achieved / peak,
-            "frac_at_held_clock": v["valu_busy_at_pmc_clock"], "clock_ghz_pmc": v["clock_ghz_pmc"],
-            "held_clock_source": "counter pass: VALU SIMD-cycles / (4 SIMDs x CUs x GRBM_GUI_ACTIVE/8), same dispatches",
+            "frac_at_held_clock": held, "clock_ghz_pmc": v.get("clock_ghz_pmc"),
+            "held_clock_source": "counter pass: VALU SIMD-cycles / (4 SIMDs x CUs x GRBM_GUI_ACTIVE/8), same dispatches"
+            if held is not None else "not in this PMC entry (written before the field existed)",
             "valu_insts_per_launch": v["SQ_INSTS_VALU"], "mean_simd_cycles_per_valu": v["mean_simd_cycles_per_valu"],
             "valu_simd_cycles_per_launch": cyc, "uncosted_opcodes": v.get("uncosted_opcodes"), "hbm": hbm}
 

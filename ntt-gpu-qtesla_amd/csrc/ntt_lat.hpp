@@ -280,6 +280,9 @@ __global__ __launch_bounds__(LatGeo<PSel<PS>::T::LOGN>::T) void k_ntt_lat(const 
     constexpr int L = P::LOGN;
     using G = LatGeo<L>;
     constexpr int GN = G::GN, NP = G::NP, R = G::R;
+    // n = 8192: 2 x 8448 words = 66 KiB, above the 64 KiB of earlier CDNA
+    // generations; gfx950 gives a workgroup up to 160 KiB
+    static_assert(2 * G::BUF * 4 <= 160 * 1024, "LDS per workgroup (gfx950: 160 KiB)");
     __shared__ uint32_t lds[2 * G::BUF];
     const uint32_t t = threadIdx.x;
     const uint32_t *src = in + (size_t)blockIdx.x * P::N;
@@ -346,6 +349,8 @@ __global__ __launch_bounds__(LatGeo<PSel<PS>::T::LOGN>::T) void k_poly_mul_lat(c
     using G = LatGeo<L>;
     static_assert(G::R == 1, "latency products: n <= 4096");
     constexpr int GN = G::GN, NP = G::NP, NF = BHAT ? 1 : 2;
+    // n = 4096 poly_mul (NF = 2): 4 x 4224 words = 66 KiB (gfx950: up to 160 KiB)
+    static_assert(2 * NF * G::BUF * 4 <= 160 * 1024, "LDS per workgroup (gfx950: 160 KiB)");
     __shared__ uint32_t lds[2 * NF * G::BUF];
     const uint32_t t = threadIdx.x;
     const size_t off = (size_t)blockIdx.x * P::N;

@@ -76,13 +76,6 @@ __host__ __device__ constexpr uint32_t latr_phys(uint32_t pos, LatPad p)
     return pos + (uint32_t)p.c1 * (pos >> 5) + (uint32_t)p.c2 * (pos >> 10);
 }
 
-#ifndef LATR_SCALAR_TW
-#define LATR_SCALAR_TW 1
-#endif
-#ifndef LATR_SETPRIO
-#define LATR_SETPRIO 0   // A/B: raise the wave priority until the polynomial's loads are issued
-#endif
-
 template <int L_, int RB_>
 struct LatRGeo {
     static constexpr int L = L_, RB = RB_;
@@ -124,40 +117,26 @@ struct LatRTw {
     static constexpr int NS = (1 << RB) - 1;   // twiddles per full pass
     uint2 w[G::NP][NS];
     static constexpr int slot(int i, int m) { return (1 << (RB - 1 - i)) - 1 + m; }
-    // A pass's twiddle indices depend on the thread through t >> g0(j) only,
-    // so with g0 >= 6 they are wave-uniform (scalar loads) and with g0 = 5
-    // they take two values per wave, by lane bit 5: both are loaded as
-    // scalars and selected per lane (LATR_SCALAR_TW; one v_cndmask per word
-    // instead of a 64-lane vector load of 2 distinct words)
+    // (A pass's twiddle indices depend on the thread through t >> g0(j) only:
+    // wave-uniform for g0 >= 6, two values per wave for g0 = 5.  Loading
+    // those as scalars, selected per lane by v_cndmask, measured no faster:
+    // p-III radix-8 fwd / inv 3.60 / 3.74 -> 3.66 / 3.72 ms per 2^20, p-I
+    // 1.67 / 1.66 -> 1.74 / 1.71 (profiles/r06/latr/ab9/); the compiler turns
+    // the uniform pass-0 indices into scalar loads by itself.)
     __device__ __forceinline__ void load(uint32_t t)
     {
         const uint2 *tw = lat_tw<PS, INV>();
-        const uint32_t tw0 = __builtin_amdgcn_readfirstlane(t) & ~63u;   // the wave's first thread
         sfor<G::NP>([&](auto JJ) {
             constexpr int j = decltype(JJ)::value;
-            constexpr int g0 = G::g0(j);
             const uint32_t p0 = G::pos(j, t, 0);
             sfor<RB>([&](auto II) {
                 constexpr int i = decltype(II)::value;
                 if constexpr (G::has(j, i)) {
-                    constexpr int b = g0 + i;
+                    constexpr int b = G::g0(j) + i;
+                    const uint32_t k0 = (1u << (L - 1 - b)) + (p0 >> (b + 1));
                     sfor<(1 << (RB - 1 - i))>([&](auto MM) {
                         constexpr int m = decltype(MM)::value;
-                        if constexpr (LATR_SCALAR_TW && g0 >= 5) {
-                            const uint32_t klo = __builtin_amdgcn_readfirstlane((1u << (L - 1 - b)) + (G::pos(j, tw0, 0) >> (b + 1)) + m);
-                            const uint2 lo = tw[klo];
-                            if constexpr (g0 >= 6) {
-                                w[j][slot(i, m)] = lo;
-                            } else {
-                                const uint32_t khi = __builtin_amdgcn_readfirstlane(
-                                    (1u << (L - 1 - b)) + (G::pos(j, tw0 | 32u, 0) >> (b + 1)) + m);
-                                const uint2 hi = tw[khi];
-                                const bool up = (t & 32u) != 0;
-                                w[j][slot(i, m)] = make_uint2(up ? hi.x : lo.x, up ? hi.y : lo.y);
-                            }
-                        } else {
-                            w[j][slot(i, m)] = tw[(1u << (L - 1 - b)) + (p0 >> (b + 1)) + m];
-                        }
+                        w[j][slot(i, m)] = tw[k0 + m];
                     });
                 }
             });
@@ -271,6 +250,8 @@ __global__ __launch_bounds__((LatRGeo<PSel<PS>::T::LOGN, RB>::T)) void k_ntt_lat
     constexpr uint32_t T = G::T;
     constexpr int NE = G::NE, NP = G::NP;
     constexpr bool ARITH = VAR == 0 || VAR == 2;
+    // n = 8192 radix-8: 2 x 9216 words = 72 KiB (gfx950: up to 160 KiB per workgroup)
+    static_assert(G::LDS_WORDS * 4 <= 160 * 1024, "LDS per workgroup (gfx950: 160 KiB)");
     __shared__ uint32_t lds[G::LDS_WORDS];
     const uint32_t t = threadIdx.x;
     const uint32_t poly = blockIdx.x;
@@ -283,7 +264,6 @@ __global__ __launch_bounds__((LatRGeo<PSel<PS>::T::LOGN, RB>::T)) void k_ntt_lat
     // natural order t + T e (the inverse's bit-reversed-order input: the last
     // forward pass's positions NE t + e)
     uint32_t v[NE];
-    if constexpr (LATR_SETPRIO) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
         if constexpr (VAR == 2) v[e] = (t * NE + e + poly) & 0xFFFFu;   // no global traffic: synthetic words
@@ -291,7 +271,6 @@ __global__ __launch_bounds__((LatRGeo<PSel<PS>::T::LOGN, RB>::T)) void k_ntt_lat
     }
     LatRTw<PS, INV, RB> W;
     if constexpr (ARITH || VAR == 3) W.load(t);
-    if constexpr (LATR_SETPRIO) __builtin_amdgcn_s_setprio(0);
     if constexpr (VAR == 3)
 #pragma unroll
         for (int j = 0; j < NP; ++j)

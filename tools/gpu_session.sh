@@ -128,6 +128,15 @@ for step in "${steps[@]}"; do
              run ab9_chk 300 python tools/ab.py $L --param p-III --batch 65536 --ops fwd,inv,fwdbr,invbr --rounds 2 &&
              run ab9_p3 300 python tools/ab.py $L --param p-III --batch 1048576 --ops fwd,inv --inplace --rounds 9 &&
              run ab9_p1 300 python tools/ab.py $L --param p-I --batch 1048576 --ops fwd,inv --inplace --rounds 9 ;;
+        # round 6: FETCH / WRITE of the one-launch bit-reversed n = 4096 / 8192
+        # transforms next to the natural-order ones (same process, ab.py)
+        pmcbr) for n in 4096 8192; do b=$((8589934592 / 4 / n)); a="tools/ab.py ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so --param p-III-$n --batch $b --ops fwd,fwdbr,inv,invbr --rounds 1";
+                   run pmcbr_${n}_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcbr_${n}_fetch -o run -- python3 $a || exit 1;
+                   run pmcbr_${n}_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcbr_${n}_write -o run -- python3 $a || exit 1; done ;;
+        # round 6: rocprofv3 kernel stats of the headline with every transform
+        # on the radix-8 / radix-16 one-polynomial-per-workgroup kernels
+        proflatr) for v in lat8 lat16; do
+                      NTT_AMD_LIB=$PWD/ntt-gpu-qtesla_amd/lib/ab8/$v.so run proflatr_$v 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/proflatr_$v -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-check || exit 1; done ;;
         sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
