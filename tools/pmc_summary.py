@@ -31,12 +31,21 @@ def load(path):
     return out
 
 
-def kernel_patterns(op, ps, ring):
+def kernel_patterns(op, ps, ring, radix=None):
+    """rocprof kernel-name patterns of a bench op's launches.  radix: the
+    small-batch family the transforms run at this batch (ntt_small_batch_radix:
+    4 / 8 / 16 = the one-polynomial-per-workgroup kernels, 0 / None = the
+    batch kernels)."""
+    if op in ("fwdinv", "fwd", "inv") and radix:
+        kern = (lambda inv: f"k_ntt_lat<{ps}, {inv}, false>") if radix == 4 else \
+            (lambda inv: f"k_ntt_latr<{ps}, {inv}, false, {3 if radix == 8 else 4}, 0>")
+        return {"fwdinv": {"fwd": kern("false"), "inv": kern("true")}, "fwd": {"fwd": kern("false")},
+                "inv": {"inv": kern("true")}}[op]
     if ps >= 3:   # n = 4096 / 8192: wave-per-polynomial transforms (and n = 4096 products),
         # the n = 8192 products on the multi-wave four-step kernel
         mk = "k_poly_mul_big" if ps == 3 else "k_poly_mul_large"
-        return {"fwdinv": {"fwd": f"k_ntt_fwd_big<{ps}>", "inv": f"k_ntt_inv_big<{ps}>"},
-                "fwd": {"fwd": f"k_ntt_fwd_big<{ps}>"}, "inv": {"inv": f"k_ntt_inv_big<{ps}>"},
+        return {"fwdinv": {"fwd": f"k_ntt_fwd_big<{ps}, false>", "inv": f"k_ntt_inv_big<{ps}, false>"},
+                "fwd": {"fwd": f"k_ntt_fwd_big<{ps}, false>"}, "inv": {"inv": f"k_ntt_inv_big<{ps}, false>"},
                 "polymul": {"mul": f"{mk}<{ps}, false>"},
                 "polymul_ntt": {"mulntt": f"{mk}<{ps}, true>"}}[op]
     return {"fwdinv": {"fwd": f"k_ntt_fwd<{ps}, false>", "inv": f"k_ntt_inv<{ps}, false>"},
@@ -68,7 +77,11 @@ def main():
     alg = batch * n * (12 if op in ("polymul", "polymul_ntt", "nussbaumer") else 8)
     f, w = load(args.fetch), load(args.write)
     kernels = {}
-    for key, pat in kernel_patterns(op, ps, ring).items():
+    radix = None
+    if op in ("fwdinv", "fwd", "inv"):
+        radices = {ntt_amd.small_batch_radix(param, k, batch) for k in bench.SWITCH_OPS[op]}
+        radix = radices.pop() if len(radices) == 1 else None
+    for key, pat in kernel_patterns(op, ps, ring, radix).items():
         fk = [v for (k, c), v in f.items() if c == "FETCH_SIZE" and pat in k]
         wk = [v for (k, c), v in w.items() if c == "WRITE_SIZE" and pat in k]
         if not fk or not wk:
