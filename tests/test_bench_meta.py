@@ -223,3 +223,32 @@ def test_native_latency_reports_instead_of_raising():
     import types
     r = bench.native_latency(types.SimpleNamespace(op="fwd", param="p-I"), 1)
     assert ("native_c_abi_us_per_call" in r) or ("native_note" in r)
+
+
+def test_final_verify_lines_carry_this_builds_counters():
+    """The newest round's re-run bench lines (profiles/rNN/final/verify/, run
+    after the PMC summary was re-stamped for the measured build) carry the
+    counters of their own build: every VALU-bound line with a VALU entry has
+    a frac and no note naming another build, every HBM-bound line a traffic
+    figure (VERDICT r05 ask 7)."""
+    import glob
+    import json
+    rounds = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "final", "verify")))
+    if not rounds:
+        pytest.skip("no final/verify lines committed")
+    lines = sorted(glob.glob(os.path.join(rounds[-1], "bench*.json")))
+    assert lines, rounds[-1]
+    hashes = set()
+    for f in lines:
+        d = json.load(open(f))
+        r = d["roofline"]
+        hashes.add(d["build"]["hash"])
+        note = r.get("valu_note") or r.get("traffic_note") or ""
+        assert "measured on build" not in note, (f, note)
+        if r["bound"] == "valu":
+            if "no VALU counter entry" in note:
+                continue   # poly_mul_ntt lines: no counter pass of their own
+            assert r["frac"] is not None and r["frac_at_held_clock"] is not None, f
+        else:
+            assert r["traffic"] is not None, f
+    assert len(hashes) == 1, hashes
