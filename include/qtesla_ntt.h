@@ -207,12 +207,14 @@ int ntt_sync_expiries(uint32_t *count);
  * run the batch kernels.  All give identical results; the thresholds are the
  * measured crossovers of their launch times, per (n, op).  The reference
  * has one launch shape for every batch (<<<BATCH, T>>>, NTT.cu:2216). */
-#define NTT_OP_FWD 0     /* poly_ntt, poly_ntt_oop       */
-#define NTT_OP_INV 1     /* poly_invntt, poly_invntt_oop */
-#define NTT_OP_FWD_BR 2  /* poly_ntt_bitrev              */
-#define NTT_OP_INV_BR 3  /* poly_invntt_bitrev           */
-#define NTT_OP_MUL 4     /* poly_mul                     */
-#define NTT_OP_MUL_NTT 5 /* poly_mul_ntt                 */
+#define NTT_OP_FWD 0     /* poly_ntt (in place; also poly_ntt_oop with d_out == d_in) */
+#define NTT_OP_INV 1     /* poly_invntt (in place; also poly_invntt_oop, d_out == d_in) */
+#define NTT_OP_FWD_BR 2  /* poly_ntt_bitrev                                           */
+#define NTT_OP_INV_BR 3  /* poly_invntt_bitrev                                        */
+#define NTT_OP_MUL 4     /* poly_mul                                                  */
+#define NTT_OP_MUL_NTT 5 /* poly_mul_ntt                                              */
+#define NTT_OP_FWD_OOP 6 /* poly_ntt_oop, distinct buffers                            */
+#define NTT_OP_INV_OOP 7 /* poly_invntt_oop, distinct buffers                         */
 int ntt_small_batch_max(int param_set, int op, size_t *max_batch);
 /* Which kernel family entry point `op` of `param_set` runs at `batch`
  * polynomials: *radix = 4 / 8 / 16 for the one-polynomial-per-workgroup

@@ -166,7 +166,8 @@ static_assert((int)FWD == (int)LAT_FWD && (int)INV == (int)LAT_INV && (int)FWD_B
                   (int)INV_BR == (int)LAT_INV_BR,
               "switch table order");
 static_assert(LAT_FWD == NTT_OP_FWD && LAT_INV == NTT_OP_INV && LAT_FWD_BR == NTT_OP_FWD_BR &&
-                  LAT_INV_BR == NTT_OP_INV_BR && LAT_MUL == NTT_OP_MUL && LAT_MUL_NTT == NTT_OP_MUL_NTT,
+                  LAT_INV_BR == NTT_OP_INV_BR && LAT_MUL == NTT_OP_MUL && LAT_MUL_NTT == NTT_OP_MUL_NTT &&
+                  LAT_FWD_OOP == NTT_OP_FWD_OOP && LAT_INV_OOP == NTT_OP_INV_OOP,
               "ABI op codes");
 
 template <int PS> struct LXform {
@@ -192,7 +193,9 @@ template <int PS> struct LXform {
             return finish_launch();
         }
 #endif
-        const int rb = k == BITREV ? 0 : lat_radix(PS, (int)k, batch);
+        // FWD / INV: in place or out of place (LAT_FWD_OOP / LAT_INV_OOP)
+        const int sop = (k == FWD || k == INV) && in != out ? (k == FWD ? LAT_FWD_OOP : LAT_INV_OOP) : (int)k;
+        const int rb = k == BITREV ? 0 : lat_radix(PS, sop, batch);
         if (rb == 2) {
             // small batches: radix-4 passes, one polynomial per n/4-thread workgroup (ntt_lat.hpp)
             const dim3 g((uint32_t)batch), b(LatGeo<PSel<PS>::T::LOGN>::T);

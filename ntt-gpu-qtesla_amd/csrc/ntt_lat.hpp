@@ -52,7 +52,14 @@ namespace qntt {
 // polynomial; at the BASELINE batches the batch kernels stay ahead (p-III
 // forward at 2^20: 3.23 ms against 3.38 / 3.50 ms radix-8 / 16, 4.77 radix-4),
 // except at n = 1024 where radix-16 (one wave per polynomial) runs level.
-enum LatOp { LAT_FWD, LAT_INV, LAT_FWD_BR, LAT_INV_BR, LAT_MUL, LAT_MUL_NTT, LAT_NOPS };
+// LAT_FWD / LAT_INV: in place (poly_ntt / poly_invntt, or the _oop calls
+// with d_out == d_in); LAT_FWD_OOP / LAT_INV_OOP: distinct buffers.  The
+// families rank differently in place: the batch kernels run 5-8 % slower in
+// place than out of place, the one-polynomial-per-workgroup kernels 0-3 %
+// faster (profiles/r06/latr/switch_sweep_inplace.json against
+// switch_sweep_latr.json), so at n = 1024 the radix-16 kernel takes every
+// in-place batch above its first tier (2^20 p-I forward: 1.55 against 1.68 ms)
+enum LatOp { LAT_FWD, LAT_INV, LAT_FWD_BR, LAT_INV_BR, LAT_MUL, LAT_MUL_NTT, LAT_FWD_OOP, LAT_INV_OOP, LAT_NOPS };
 struct LatTier {
     int rb0;
     size_t max0;
@@ -68,13 +75,14 @@ constexpr LatTier lat_tier(int ps, int op)
                                                                                     : LatTier{2, ~(size_t)0, 2, 0};
 }
 #else
+constexpr size_t kAll = 0x7FFFFFFF;   // every batch the ABI accepts
 constexpr LatTier kLatTier[5][LAT_NOPS] = {
-    // fwd                     inv                        fwd_br                  inv_br                   mul              mul_ntt
-    {{2, 1024, 4, 262144}, {2, 1024, 4, 262144}, {2, 1024, 3, 4096}, {2, 1024, 3, 32768}, {2, 2816, 0, 0}, {2, 5120, 0, 0}},   // ref
-    {{2, 1024, 4, 262144}, {2, 1024, 4, 262144}, {2, 1024, 3, 4096}, {2, 1024, 3, 32768}, {2, 2816, 0, 0}, {2, 5120, 0, 0}},   // p-I
-    {{3, 65536, 0, 0}, {3, 32768, 0, 0}, {3, 2048, 0, 0}, {3, 2048, 0, 0}, {2, 1280, 0, 0}, {2, 1792, 0, 0}},                  // p-III
-    {{4, 16384, 0, 0}, {3, 32768, 0, 0}, {3, 2048, 0, 0}, {3, 16384, 0, 0}, {2, 512, 0, 0}, {2, 512, 0, 0}},                   // n = 4096
-    {{4, 32768, 0, 0}, {4, 32768, 0, 0}, {4, 1024, 0, 0}, {3, 16384, 0, 0}, {2, 0, 0, 0}, {2, 0, 0, 0}},                       // n = 8192
+    // fwd (in place)         inv (in place)         fwd_br               inv_br                mul              mul_ntt          fwd_oop                inv_oop
+    {{2, 1024, 4, kAll}, {2, 1024, 4, kAll}, {2, 1024, 3, 4096}, {2, 1024, 3, 32768}, {2, 2816, 0, 0}, {2, 5120, 0, 0}, {2, 1024, 4, 262144}, {2, 1024, 4, 262144}},  // ref
+    {{2, 1024, 4, kAll}, {2, 1024, 4, kAll}, {2, 1024, 3, 4096}, {2, 1024, 3, 32768}, {2, 2816, 0, 0}, {2, 5120, 0, 0}, {2, 1024, 4, 262144}, {2, 1024, 4, 262144}},  // p-I
+    {{3, 131072, 0, 0}, {3, 65536, 0, 0}, {3, 2048, 0, 0}, {3, 2048, 0, 0}, {2, 1280, 0, 0}, {2, 1792, 0, 0}, {3, 65536, 0, 0}, {3, 32768, 0, 0}},                  // p-III
+    {{4, 16384, 0, 0}, {4, 16384, 0, 0}, {3, 2048, 0, 0}, {3, 16384, 0, 0}, {2, 512, 0, 0}, {2, 512, 0, 0}, {4, 16384, 0, 0}, {3, 32768, 0, 0}},                     // n = 4096
+    {{4, 32768, 0, 0}, {4, 32768, 0, 0}, {4, 1024, 0, 0}, {3, 16384, 0, 0}, {2, 0, 0, 0}, {2, 0, 0, 0}, {4, 32768, 0, 0}, {4, 32768, 0, 0}},                         // n = 8192
 };
 constexpr LatTier lat_tier(int ps, int op) { return kLatTier[ps][op]; }
 #endif

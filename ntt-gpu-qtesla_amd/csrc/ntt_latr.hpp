@@ -76,6 +76,10 @@ __host__ __device__ constexpr uint32_t latr_phys(uint32_t pos, LatPad p)
     return pos + (uint32_t)p.c1 * (pos >> 5) + (uint32_t)p.c2 * (pos >> 10);
 }
 
+#ifndef LATR_JIT_TW
+#define LATR_JIT_TW 0   // A/B: load each pass's twiddles after the previous pass's butterflies
+#endif
+
 template <int L_, int RB_>
 struct LatRGeo {
     static constexpr int L = L_, RB = RB_;
@@ -123,24 +127,28 @@ struct LatRTw {
     // p-III radix-8 fwd / inv 3.60 / 3.74 -> 3.66 / 3.72 ms per 2^20, p-I
     // 1.67 / 1.66 -> 1.74 / 1.71 (profiles/r06/latr/ab9/); the compiler turns
     // the uniform pass-0 indices into scalar loads by itself.)
+    // pass j's twiddles; `anchor` (0) is an opaque value the caller derives
+    // from the data, so the loads cannot be hoisted above that point
+    template <int j>
+    __device__ __forceinline__ void load_pass(uint32_t t, uint32_t anchor = 0)
+    {
+        const uint2 *tw = lat_tw<PS, INV>() + anchor;
+        const uint32_t p0 = G::pos(j, t, 0);
+        sfor<RB>([&](auto II) {
+            constexpr int i = decltype(II)::value;
+            if constexpr (G::has(j, i)) {
+                constexpr int b = G::g0(j) + i;
+                const uint32_t k0 = (1u << (L - 1 - b)) + (p0 >> (b + 1));
+                sfor<(1 << (RB - 1 - i))>([&](auto MM) {
+                    constexpr int m = decltype(MM)::value;
+                    w[j][slot(i, m)] = tw[k0 + m];
+                });
+            }
+        });
+    }
     __device__ __forceinline__ void load(uint32_t t)
     {
-        const uint2 *tw = lat_tw<PS, INV>();
-        sfor<G::NP>([&](auto JJ) {
-            constexpr int j = decltype(JJ)::value;
-            const uint32_t p0 = G::pos(j, t, 0);
-            sfor<RB>([&](auto II) {
-                constexpr int i = decltype(II)::value;
-                if constexpr (G::has(j, i)) {
-                    constexpr int b = G::g0(j) + i;
-                    const uint32_t k0 = (1u << (L - 1 - b)) + (p0 >> (b + 1));
-                    sfor<(1 << (RB - 1 - i))>([&](auto MM) {
-                        constexpr int m = decltype(MM)::value;
-                        w[j][slot(i, m)] = tw[k0 + m];
-                    });
-                }
-            });
-        });
+        sfor<G::NP>([&](auto JJ) { load_pass<decltype(JJ)::value>(t); });
     }
 };
 
@@ -164,9 +172,19 @@ __device__ __forceinline__ void latr_xchg(uint32_t (&v)[NE], uint32_t *lds, int 
 // forward CT passes (natural-order groups of pass 0 in; the last pass's
 // groups out, position pos holding X[brv(pos)], values in [0, 4q));
 // exchanges 0 .. NP-2
-template <int PS, int RB, bool ARITH = true>
-__device__ __forceinline__ void latr_fwd(uint32_t (&v)[1 << RB], const LatRTw<PS, false, RB> &W, uint32_t *lds,
-                                         uint32_t t)
+// JIT: pass j+1's twiddles are loaded after pass j's butterflies (in flight
+// during the exchange), so only one pass's twiddles are live at a time;
+// otherwise the caller has loaded every pass's up front.
+template <class V>
+__device__ __forceinline__ uint32_t latr_anchor(const V &v)
+{
+    uint32_t a = 0;
+    asm volatile("" : "+v"(a) : "v"(v[0]), "v"(v[sizeof(V) / sizeof(v[0]) - 1]));
+    return a;
+}
+
+template <int PS, int RB, bool ARITH = true, bool JIT = false>
+__device__ __forceinline__ void latr_fwd(uint32_t (&v)[1 << RB], LatRTw<PS, false, RB> &W, uint32_t *lds, uint32_t t)
 {
     using P = typename PSel<PS>::T;
     using G = LatRGeo<P::LOGN, RB>;
@@ -185,6 +203,7 @@ __device__ __forceinline__ void latr_fwd(uint32_t (&v)[1 << RB], const LatRTw<PS
                 }
             }
         });
+        if constexpr (ARITH && JIT && j + 1 < G::NP) W.template load_pass<j + 1>(t, latr_anchor(v));
         if constexpr (j + 1 < G::NP) {
             constexpr LatPad pd = latr_pad(G::L, RB, false, j);
             latr_xchg<G>(v, lds, j, latr_phys(G::pos(j, t, 0), pd),
@@ -197,9 +216,9 @@ __device__ __forceinline__ void latr_fwd(uint32_t (&v)[1 << RB], const LatRTw<PS
 // inverse GS passes from the last pass's groups (inputs in [0, 2q)) to pass
 // 0's natural-order groups, the last stage scaled by S0 (x + y) and S1
 // (x - y); canonical outputs.  Exchanges x0 + 1 .. x0 + NP - 1.
-template <int PS, int RB, uint32_t S0, uint32_t S1, bool ARITH = true>
-__device__ __forceinline__ void latr_inv(uint32_t (&v)[1 << RB], const LatRTw<PS, true, RB> &W, uint32_t *lds,
-                                         uint32_t t, int x0)
+template <int PS, int RB, uint32_t S0, uint32_t S1, bool ARITH = true, bool JIT = false>
+__device__ __forceinline__ void latr_inv(uint32_t (&v)[1 << RB], LatRTw<PS, true, RB> &W, uint32_t *lds, uint32_t t,
+                                         int x0)
 {
     using P = typename PSel<PS>::T;
     using G = LatRGeo<P::LOGN, RB>;
@@ -217,6 +236,7 @@ __device__ __forceinline__ void latr_inv(uint32_t (&v)[1 << RB], const LatRTw<PS
                 }
             }
         });
+        if constexpr (ARITH && JIT && j > 0) W.template load_pass<j - 1>(t, latr_anchor(v));
         if constexpr (j > 0) {
             constexpr LatPad pd = latr_pad(G::L, RB, true, j - 1);
             latr_xchg<G>(v, lds, x0 + G::NP - j, latr_phys(G::pos(j, t, 0), pd),
@@ -270,14 +290,16 @@ __global__ __launch_bounds__((LatRGeo<PSel<PS>::T::LOGN, RB>::T)) void k_ntt_lat
         else v[e] = ld_in(src + (INV && BR ? NE * t + e : t + T * e));
     }
     LatRTw<PS, INV, RB> W;
-    if constexpr (ARITH || VAR == 3) W.load(t);
+    constexpr bool JIT = LATR_JIT_TW;
+    if constexpr (ARITH && JIT) W.template load_pass<INV ? NP - 1 : 0>(t);
+    else if constexpr (ARITH || VAR == 3) W.load(t);
     if constexpr (VAR == 3)
 #pragma unroll
         for (int j = 0; j < NP; ++j)
 #pragma unroll
             for (int i = 0; i < LatRTw<PS, INV, RB>::NS; ++i) v[i % NE] ^= W.w[j][i].x ^ W.w[j][i].y;
     if constexpr (!INV) {
-        latr_fwd<PS, RB, ARITH>(v, W, lds, t);
+        latr_fwd<PS, RB, ARITH, JIT>(v, W, lds, t);
         if constexpr (ARITH)
 #pragma unroll
             for (int e = 0; e < NE; ++e) v[e] = canon4<P>(v[e]);
@@ -305,7 +327,7 @@ __global__ __launch_bounds__((LatRGeo<PSel<PS>::T::LOGN, RB>::T)) void k_ntt_lat
             latr_xchg<G>(v, lds, 0, latr_phys(bt, pd), [&](int e) { return latr_phys(lat_brv(e, RB), pd); },
                          latr_phys(NE * t, pd), [&](int e) { return latr_phys(e, pd); });
         }
-        latr_inv<PS, RB, P::NINV, P::C1, ARITH>(v, W, lds, t, BR ? -1 : 0);
+        latr_inv<PS, RB, P::NINV, P::C1, ARITH, JIT>(v, W, lds, t, BR ? -1 : 0);
 #pragma unroll
         for (int e = 0; e < NE; ++e) store(dst + t + T * e, v[e]);
     }

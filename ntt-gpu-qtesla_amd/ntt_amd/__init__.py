@@ -155,7 +155,7 @@ def sync_expiries() -> int:
 
 
 # entry points of the small-batch switch (NTT_OP_* in qtesla_ntt.h)
-SWITCH_OPS = {"fwd": 0, "inv": 1, "fwd_br": 2, "inv_br": 3, "mul": 4, "mul_ntt": 5}
+SWITCH_OPS = {"fwd": 0, "inv": 1, "fwd_br": 2, "inv_br": 3, "mul": 4, "mul_ntt": 5, "fwd_oop": 6, "inv_oop": 7}
 
 
 def small_batch_max(param_set, op: str) -> int:

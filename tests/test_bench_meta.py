@@ -210,9 +210,9 @@ def test_switch_table_in_library(ntt):
     v = ctypes.c_size_t()
     r = ctypes.c_int()
     assert L.ntt_small_batch_max(7, 0, ctypes.byref(v)) == ntt.NTT_ERR_PARAM
-    assert L.ntt_small_batch_max(0, 6, ctypes.byref(v)) == ntt.NTT_ERR_PARAM
+    assert L.ntt_small_batch_max(0, 8, ctypes.byref(v)) == ntt.NTT_ERR_PARAM
     assert L.ntt_small_batch_max(0, 0, None) == ntt.NTT_ERR_NULL
-    assert L.ntt_small_batch_radix(0, 6, 1, ctypes.byref(r)) == ntt.NTT_ERR_PARAM
+    assert L.ntt_small_batch_radix(0, 8, 1, ctypes.byref(r)) == ntt.NTT_ERR_PARAM
     assert L.ntt_small_batch_radix(0, 0, 1, None) == ntt.NTT_ERR_NULL
 
 

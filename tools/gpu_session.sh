@@ -137,6 +137,16 @@ for step in "${steps[@]}"; do
         # on the radix-8 / radix-16 one-polynomial-per-workgroup kernels
         proflatr) for v in lat8 lat16; do
                       NTT_AMD_LIB=$PWD/ntt-gpu-qtesla_amd/lib/ab8/$v.so run proflatr_$v 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/proflatr_$v -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-check || exit 1; done ;;
+        ab10) L="ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so ntt-gpu-qtesla_amd/lib/ab10/*.so";
+              run ab10_chk 300 python tools/ab.py $L --param p-III --batch 65536 --ops fwd,inv,fwdbr,invbr --rounds 2 &&
+              run ab10_chk1 300 python tools/ab.py $L --param p-I --batch 65536 --ops fwd,inv,fwdbr,invbr --rounds 2 &&
+              run ab10_p1s 300 python tools/ab.py $L --param p-I --batch 65536 --ops fwd,inv --inplace --rounds 31 &&
+              run ab10_p3 300 python tools/ab.py $L --param p-III --batch 1048576 --ops fwd,inv --inplace --rounds 9 &&
+              run ab10_p1 300 python tools/ab.py $L --param p-I --batch 1048576 --ops fwd,inv --inplace --rounds 9 &&
+              run ab10_4096 300 python tools/ab.py $L --param p-III-4096 --batch 16384 --ops fwd,inv --inplace --rounds 31 &&
+              run ab10_8192 300 python tools/ab.py $L --param p-III-8192 --batch 32768 --ops fwd,inv --inplace --rounds 31 ;;
+        sweepip) run sweepip 900 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so ntt-gpu-qtesla_amd/lib/ab10/r8.so ntt-gpu-qtesla_amd/lib/ab10/r16.so --ops fwd,inv --inplace --rounds 5 --out gpurun_out/switch_sweep_inplace.json ;;
+        benchp1) run benchp1 300 python bench.py --op fwdinv --param p-I --batch 1048576 --steps 20 --warmup 3 --no-cpu-baseline ;;
         sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--min-batch", type=int, default=64)
     ap.add_argument("--max-batch", type=int, default=0, help="cap (0: MAX_BATCH per n)")
     ap.add_argument("--target-ms", type=float, default=2.0)
+    ap.add_argument("--inplace", action="store_true",
+                    help="fwd / inv in place (poly_ntt / poly_invntt, as bench.py runs them); default out of place")
     ap.add_argument("--out", default=None)
     ap.add_argument("--refine", default=None,
                     help="a previous sweep's JSON: time 8 points per octave inside each (n, op)'s crossover octave")
@@ -89,10 +91,11 @@ def main():
                     b *= 2
             for b in batches:
                 def launch(L, op=op, b=b):
+                    dst = x if args.inplace else z
                     if op == "fwd":
-                        rc = L.poly_ntt_oop(z.data_ptr(), x.data_ptr(), b, ps, sp)
+                        rc = L.poly_ntt_oop(dst.data_ptr(), x.data_ptr(), b, ps, sp)
                     elif op == "inv":
-                        rc = L.poly_invntt_oop(z.data_ptr(), x.data_ptr(), b, ps, sp)
+                        rc = L.poly_invntt_oop(dst.data_ptr(), x.data_ptr(), b, ps, sp)
                     elif op == "fwdbr":
                         rc = L.poly_ntt_bitrev(z.data_ptr(), x.data_ptr(), b, ps, sp)
                     elif op == "invbr":
@@ -104,11 +107,17 @@ def main():
                     if rc != 0:
                         raise RuntimeError(f"{op} b={b} rc={rc}")
                 sig = {}
+                if args.inplace and op in ("fwd", "inv"):
+                    x0 = x[: b * n].clone()
                 for tag, L in libs.items():
+                    if args.inplace and op in ("fwd", "inv"):
+                        x[: b * n].copy_(x0)
                     launch(L)
                     torch.cuda.synchronize()
-                    sig[tag] = z[: b * n: 4099].clone()
+                    sig[tag] = (x if args.inplace and op in ("fwd", "inv") else z)[: b * n: 4099].clone()
                 same = all(bool(torch.equal(sig["batch"], v)) for v in sig.values())
+                if args.inplace and op in ("fwd", "inv"):
+                    del x0
                 # one probe launch of the batch build sizes K
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
@@ -156,7 +165,7 @@ def main():
             first = next(t for t in libs if t != "batch")
             ent["lat_wins_through"] = ent[first]["wins_through"]
             summary[f"{param}:{op}"] = ent
-    out = {"rounds": args.rounds, "libs": {"batch": args.batch_lib, "small": args.lat_lib},
+    out = {"rounds": args.rounds, "inplace": args.inplace, "libs": {"batch": args.batch_lib, "small": args.lat_lib},
            "results": {p: {o: {str(b): v for b, v in pts.items()} for o, pts in ops.items()} for p, ops in res.items()},
            "summary": summary}
     txt = json.dumps(out, indent=1)
