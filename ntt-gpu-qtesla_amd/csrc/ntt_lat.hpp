@@ -54,11 +54,13 @@ namespace qntt {
 // except at n = 1024 where radix-16 (one wave per polynomial) runs level.
 // LAT_FWD / LAT_INV: in place (poly_ntt / poly_invntt, or the _oop calls
 // with d_out == d_in); LAT_FWD_OOP / LAT_INV_OOP: distinct buffers.  The
-// families rank differently in place: the batch kernels run 5-8 % slower in
-// place than out of place, the one-polynomial-per-workgroup kernels 0-3 %
-// faster (profiles/r06/latr/switch_sweep_inplace.json against
-// switch_sweep_latr.json), so at n = 1024 the radix-16 kernel takes every
-// in-place batch above its first tier (2^20 p-I forward: 1.55 against 1.68 ms)
+// families rank differently in place: the batch kernels run 2-3 % slower in
+// place than out of place, the one-polynomial-per-workgroup kernels the same
+// (one process: p-I forward at 2^20 1.686 / 1.649 ms against radix-16 1.593 /
+// 1.600, profiles/r06/latr/floorio_*.log; the in-place and out-of-place
+// sweeps, switch_sweep_inplace.json / switch_sweep_latr.json, ran on two
+// boxes), so at n = 1024 the radix-16 kernel takes every in-place batch above
+// its first tier
 enum LatOp { LAT_FWD, LAT_INV, LAT_FWD_BR, LAT_INV_BR, LAT_MUL, LAT_MUL_NTT, LAT_FWD_OOP, LAT_INV_OOP, LAT_NOPS };
 struct LatTier {
     int rb0;

@@ -147,6 +147,10 @@ for step in "${steps[@]}"; do
               run ab10_8192 300 python tools/ab.py $L --param p-III-8192 --batch 32768 --ops fwd,inv --inplace --rounds 31 ;;
         sweepip) run sweepip 900 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so ntt-gpu-qtesla_amd/lib/ab10/r8.so ntt-gpu-qtesla_amd/lib/ab10/r16.so --ops fwd,inv --inplace --rounds 5 --out gpurun_out/switch_sweep_inplace.json ;;
         benchp1) run benchp1 300 python bench.py --op fwdinv --param p-I --batch 1048576 --steps 20 --warmup 3 --no-cpu-baseline ;;
+        floorio) run floorio_p1 300 python tools/latr_floor.py --param p-I &&
+                 run floorio_p1oop 300 python tools/latr_floor.py --param p-I --oop &&
+                 run floorio_p3 300 python tools/latr_floor.py --param p-III &&
+                 run floorio_p3oop 300 python tools/latr_floor.py --param p-III --oop ;;
         sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--oop", action="store_true", help="write to a second buffer (default: in place, as bench.py)")
     args = ap.parse_args()
     import torch
     import ntt_amd
@@ -39,6 +40,7 @@ def main():
     n = ntt_amd.param_info(args.param)["n"]
     x = torch.empty(args.batch * n, dtype=torch.int32, device="cuda")
     ntt_amd.fill_uniform(x, args.param, 5)
+    y = torch.empty_like(x) if args.oop else x
     s = torch.cuda.current_stream()
     cases = {"batch_fwd_full": (0, 0), "batch_fwd_mem": (0, 3), "batch_inv_full": (1, 0), "batch_inv_mem": (1, 3)}
     for op, nm in ((5, "r8"), (6, "r16")):
@@ -47,7 +49,7 @@ def main():
                 cases[f"{nm}_{d}_{kind}"] = (op, base + v)
 
     def run(op, var):
-        rc = D.ntt_debug_variant(op, var, vp(x.data_ptr()), vp(x.data_ptr()), args.batch, ps, vp(s.cuda_stream))
+        rc = D.ntt_debug_variant(op, var, vp(y.data_ptr()), vp(x.data_ptr()), args.batch, ps, vp(s.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"variant {op}/{var}: {rc}")
     for c in cases.values():
@@ -67,6 +69,7 @@ def main():
     out = {k: {"ms": round(statistics.median(v), 4), "frac_of_8TBs": round(alg / (statistics.median(v) * 1e-3) / 8e12, 4)}
            for k, v in t.items()}
     print(json.dumps({"param": args.param, "batch": args.batch, "steps": args.steps, "rounds": args.rounds,
+                      "inplace": not args.oop,
                       "results": out}, indent=1))
 
 
