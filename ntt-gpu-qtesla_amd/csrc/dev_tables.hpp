@@ -14,6 +14,7 @@
 #include "ntt_device.hpp"
 #include "ntt_large.hpp"
 #include "ntt_big.hpp"
+#include "ntt_eo.hpp"
 #include "ntt_lat.hpp"
 #include "params.hpp"
 
@@ -212,6 +213,40 @@ inline hipError_t upload_device_tables(const Tables *tabs /* [NPARAM_SETS] */)
         hipError_t e = upload_large_tables(ps, tabs[ps]);
         if (e != hipSuccess) return e;
         if ((e = upload_big_tables(ps, tabs[ps])) != hipSuccess) return e;
+#ifdef NTT_EO
+        if (ps == LARGE_PS0 + 1) {
+            // n = 8192 even/odd combine (ntt_eo.hpp): w_k = psi^(2k+1), CT index 4096 + brv12(k)
+            std::vector<uint32_t> c(2 * 2 * 4096);
+            for (int inv = 0; inv < 2; inv++)
+                for (uint32_t k = 0; k < 4096; k++)
+                    dev_pair(*param_set(ps), tabs[ps], inv != 0, 4096u + bitrev(k, 12), c[(inv * 4096 + k) * 2],
+                             c[(inv * 4096 + k) * 2 + 1]);
+            if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_eotw), c.data(), c.size() * 4, 0, hipMemcpyHostToDevice)) != hipSuccess)
+                return e;
+            // the split form: lambda_l = psi^(+-2 l) (Shoup pairs), mu = psi^(+-(2 k0 + 1)),
+            // k0 = 128 brv5(I) + 64 c + 128 par (ntt_eo.hpp, EO_TWJIT)
+            const ParamSet &p8 = *param_set(ps);
+            const Tables &t8 = tabs[ps];
+            uint2 lam[2][64], mu[2][2][2][16];
+            for (int inv = 0; inv < 2; inv++) {
+                const uint32_t g = inv ? t8.inv[2 * 4096] : t8.fwd[2 * 4096];   // psi^(+-1)
+                const uint32_t g2 = (uint32_t)((uint64_t)g * g % p8.q);
+                uint64_t x = 1;
+                for (uint32_t l = 0; l < 64; l++, x = x * g2 % p8.q) {
+                    lam[inv][l].x = (uint32_t)x;
+                    lam[inv][l].y = shoup((uint32_t)x, p8.q);
+                }
+                for (uint32_t par = 0; par < 2; par++)
+                    for (uint32_t cc = 0; cc < 2; cc++)
+                        for (uint32_t i = 0; i < 16; i++) {
+                            const uint32_t k0 = 128u * bitrev(i, 5) + 64u * cc + 128u * par;
+                            dev_pair(p8, t8, inv != 0, 4096u + bitrev(k0, 12), mu[inv][par][cc][i].x, mu[inv][par][cc][i].y);
+                        }
+            }
+            if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_eolam), lam, sizeof lam, 0, hipMemcpyHostToDevice)) != hipSuccess) return e;
+            if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_eomu), mu, sizeof mu, 0, hipMemcpyHostToDevice)) != hipSuccess) return e;
+        }
+#endif
         // full n-point tables of the latency kernels (ntt_lat.hpp)
         for (int inv = 0; inv < 2; inv++) {
             const std::vector<uint32_t> c = dev_const_table(*param_set(ps), tabs[ps], inv != 0);

@@ -248,9 +248,11 @@ __device__ __forceinline__ void big_fwd(uint32_t (&r)[BG::R], uint32_t *buf, con
 // pos BMIN, WIDE0: inv_pass2's wide first stage), GS pass 2 and the transpose
 // back; then the GS bit-5 stage and swap, the GS stages on pos 6 .. L-2 and
 // the last one scaled by S0 (x + y) and S1 (x - y), canonical.
-template <class BG, int BMIN, bool WIDE0, uint32_t S0, uint32_t S1V, class Source>
-__device__ __forceinline__ void big_inv(uint32_t (&r)[BG::R], uint32_t *buf, const uint2 *tab, uint32_t h, uint32_t lane,
-                                        Source &&source, uint32_t *dpoly)
+// store(J, x) takes layout-A register J's canonical result (big_inv: at
+// dpoly + 64 J + lane; ntt_eo.hpp: one parity of an n = 8192 polynomial).
+template <class BG, int BMIN, bool WIDE0, uint32_t S0, uint32_t S1V, class Source, class Store>
+__device__ __forceinline__ void big_inv_to(uint32_t (&r)[BG::R], uint32_t *buf, const uint2 *tab, uint32_t h, uint32_t lane,
+                                           Source &&source, Store &&store)
 {
     using P = typename BG::P;
     constexpr int M = BG::M, H = BG::H;
@@ -296,14 +298,23 @@ __device__ __forceinline__ void big_inv(uint32_t (&r)[BG::R], uint32_t *buf, con
     // last stage (pos L-1): x' = (x + y) S0, y' = (x - y) S1 (S1 = S0 psi^-brv(1))
     constexpr uint32_t S0P = cshoup(S0, P::Q);
     constexpr TwPair S1 = csigned_tw(S1V, P::Q);
-    uint32_t lo = lane;
-    asm volatile("" : "+v"(lo));
-    uint32_t *const dst = dpoly + lo;
     sfor<H>([&](auto J) {
         constexpr int j = J;
         const uint32_t x = r[j], y = r[j + H];
-        st_out(dst + 64u * j, csub<P::Q>(shoup_mul<P::Q>(x + y, S0, S0P)));
-        st_out(dst + 64u * (j + H), csub<P::Q>(sshoup_mul<P::Q>(x - y, S1.x, S1.y)));
+        store(J, csub<P::Q>(shoup_mul<P::Q>(x + y, S0, S0P)));
+        store(std::integral_constant<int, j + H>{}, csub<P::Q>(sshoup_mul<P::Q>(x - y, S1.x, S1.y)));
+    });
+}
+template <class BG, int BMIN, bool WIDE0, uint32_t S0, uint32_t S1V, class Source>
+__device__ __forceinline__ void big_inv(uint32_t (&r)[BG::R], uint32_t *buf, const uint2 *tab, uint32_t h, uint32_t lane,
+                                        Source &&source, uint32_t *dpoly)
+{
+    // layout A stores: lane-contiguous 256-B runs
+    uint32_t lo = lane;
+    asm volatile("" : "+v"(lo));
+    uint32_t *const dst = dpoly + lo;
+    big_inv_to<BG, BMIN, WIDE0, S0, S1V>(r, buf, tab, h, lane, source, [&](auto J, uint32_t x) __attribute__((always_inline)) {
+        st_out(dst + 64u * (uint32_t)J, x);
     });
 }
 

@@ -15,6 +15,7 @@
 #include "ntt_device.hpp"
 #include "ntt_large.hpp"
 #include "ntt_big.hpp"
+#include "ntt_eo.hpp"
 #include "ntt_lat.hpp"
 #include "ntt_latr.hpp"
 #include "ntt_internal.h"
@@ -220,6 +221,17 @@ template <int PS> struct LXform {
             ppw = ppw < 1 ? 1 : (ppw > NTT_PPW_MAX ? NTT_PPW_MAX : ppw);
             const dim3 g((uint32_t)((batch + BG::WAVES * ppw - 1) / (BG::WAVES * ppw))), b(BG::NT);
             const uint32_t pw = (uint32_t)ppw;
+#ifdef NTT_EO
+            if (PS == LARGE_PS0 + 1 && (k == FWD || k == INV)) {
+                // n = 8192 as two n = 4096 halves, a pair of waves per polynomial (ntt_eo.hpp)
+                size_t pe = batch / ((size_t)EO::NPAIR * d.cus * 2);
+                pe = pe < 1 ? 1 : (pe > NTT_PPW_MAX ? NTT_PPW_MAX : pe);
+                const dim3 ge((uint32_t)((batch + EO::NPAIR * pe - 1) / (EO::NPAIR * pe))), be(EO::BG::NT);
+                if (k == FWD) hipLaunchKernelGGL(k_ntt_fwd_eo, ge, be, 0, s, in, out, nb, (uint32_t)pe);
+                else hipLaunchKernelGGL(k_ntt_inv_eo, ge, be, 0, s, in, out, nb, (uint32_t)pe);
+                return finish_launch();
+            }
+#endif
             switch (k) {
             case FWD: hipLaunchKernelGGL((k_ntt_fwd_big<PS, false>), g, b, 0, s, in, out, nb, pw); break;
             case INV: hipLaunchKernelGGL((k_ntt_inv_big<PS, false>), g, b, 0, s, in, out, nb, pw); break;

@@ -151,6 +151,11 @@ for step in "${steps[@]}"; do
                  run floorio_p1oop 300 python tools/latr_floor.py --param p-I --oop &&
                  run floorio_p3 300 python tools/latr_floor.py --param p-III &&
                  run floorio_p3oop 300 python tools/latr_floor.py --param p-III --oop ;;
+        ab11) L="ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so ntt-gpu-qtesla_amd/lib/ab11/*.so";
+              run ab11_chk37 120 python tools/ab.py $L --param p-III-8192 --batch 32805 --ops fwd,inv --rounds 1 &&
+              run ab11_chk 300 python tools/ab.py $L --param p-III-8192 --batch 40001 --ops fwd,inv --rounds 2 &&
+              run ab11_8192 300 python tools/ab.py $L --param p-III-8192 --batch 262144 --ops fwd,inv --inplace --rounds 9 &&
+              run ab11_8192s 300 python tools/ab.py $L --param p-III-8192 --batch 65536 --ops fwd,inv --inplace --rounds 15 ;;
         sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
