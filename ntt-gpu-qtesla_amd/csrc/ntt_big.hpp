@@ -123,6 +123,34 @@ __device__ __forceinline__ uint32_t big_wbase(uint32_t lane)
     return ((lane & 31u) ^ (h << 4)) + 1024u * h;
 }
 
+// Buffer-resource access (scalar base, one 32-bit VGPR offset, the constant
+// part of each offset in an SGPR, `bytes` the bound: accesses past it are
+// dropped / read 0; POL: cache policy, 2 = nontemporal).  A region wider than
+// the 8 KiB immediate range takes one 64-bit VGPR base per 8 KiB as global
+// addresses (ntt_eo.hpp: held across its loop, they spilled).  The one-wave
+// n = 8192 kernels measured no faster with them (4.27 / 4.33 against 4.24 /
+// 4.27 ms per 2^18, profiles/r06/big8192), nor at 12 waves (4.75 / 5.54 ms:
+// 168 VGPRs leave 32 / 171 spilled), so they keep global addresses.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
+}
+template <int POL = 2>
+__device__ __forceinline__ void buf_st(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, POL);
+}
+template <int POL = 2>
+__device__ __forceinline__ uint32_t buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
+{
+    return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, POL);
+}
+__device__ __forceinline__ uint2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
+{
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    return make_uint2(x[0], x[1]);
+}
+
 // the R words of a lane at compile-time offsets from one base pointer
 template <int NR, class Off>
 __device__ __forceinline__ void load32n(uint32_t (&r)[NR], const uint32_t *src, Off off)
@@ -433,9 +461,7 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const
         }
     };
     auto process = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
-        big_inv<BG, 0, false, BG::PL::NINV, BG::PL::C1>(
-            r, buf, tab, h, lane,
-            [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {
+        auto source = [&](auto C, uint32_t (&v)[32]) __attribute__((always_inline)) {
                 if constexpr (!BR) {
                     sfor<32>([&](auto JP) { v[JP] = r[BG::creg(C, JP)]; });
                 } else {
@@ -453,8 +479,8 @@ __global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_ntt_inv_big(const
                     });
                     compiler_fence();
                 }
-            },
-            out + (size_t)u * N);
+        };
+        big_inv<BG, 0, false, BG::PL::NINV, BG::PL::C1>(r, buf, tab, h, lane, source, out + (size_t)u * N);
     };
     big_loop<BG>(npoly, ppw, prologue, load, process);
 }

@@ -90,14 +90,6 @@ __device__ __forceinline__ void eo_wait(const uint32_t *flag, uint32_t v)
     compiler_fence();
 }
 
-// Buffer-resource access (scalar base, one 32-bit VGPR offset, the constant
-// part of each offset in an SGPR): the pair's words span 32 KiB, which as
-// global addresses takes a 64-bit VGPR base per 8 KiB -- held across the
-// loop, they spilled.  `bytes` = 0 drops every store (a pair past the batch).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t eo_rsrc(const void *base, uint32_t bytes)
-{
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
-}
 // cache policy: 2 = nontemporal.  The stride-2 accesses (one parity of a
 // polynomial) share every cache line with the partner wave
 #ifndef EO_POL_S2
@@ -106,21 +98,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t eo_rsrc(const void *base, uint
 #ifndef EO_POL_C
 #define EO_POL_C 2
 #endif
-template <int POL>
-__device__ __forceinline__ void eo_st(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
-{
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, POL);
-}
-template <int POL>
-__device__ __forceinline__ uint32_t eo_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
-{
-    return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, POL);
-}
-__device__ __forceinline__ uint2 eo_ldtw(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
-{
-    const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
-    return make_uint2(x[0], x[1]);
-}
 
 __global__ __launch_bounds__(EO::BG::NT, EO::BG::OCC) void k_ntt_fwd_eo(const uint32_t *in, uint32_t *out, uint32_t npoly,
                                                                       uint32_t ppw)
@@ -146,8 +123,8 @@ __global__ __launch_bounds__(EO::BG::NT, EO::BG::OCC) void k_ntt_fwd_eo(const ui
     auto load = [&](uint32_t q) __attribute__((always_inline)) {
         uint32_t lo = 2u * lane + par;
         asm volatile("" : "+v"(lo));
-        const auto src = eo_rsrc(in + (size_t)q * EO::N, q < npoly ? EO::N * 4u : 0u);
-        sfor<BG::R>([&](auto J) { r[J] = eo_ld<EO_POL_S2>(src, 4u * lo, 4u * 128u * (uint32_t)J); });
+        const auto src = buf_rsrc(in + (size_t)q * EO::N, q < npoly ? EO::N * 4u : 0u);
+        sfor<BG::R>([&](auto J) { r[J] = buf_ld<EO_POL_S2>(src, 4u * lo, 4u * 128u * (uint32_t)J); });
     };
     load(p);
     fill_big_tw<BG, false>(tabw);
@@ -161,8 +138,8 @@ __global__ __launch_bounds__(EO::BG::NT, EO::BG::OCC) void k_ntt_fwd_eo(const ui
             // per-lane addresses held across the loop)
             uint32_t lo = 128u * par + lane;
             asm volatile("" : "+v"(lo));
-            const auto dst = eo_rsrc(out + (size_t)p * EO::N, EO::N * 4u);
-            const auto wt = eo_rsrc(g_eotw[0], 4096u * 8u);
+            const auto dst = buf_rsrc(out + (size_t)p * EO::N, EO::N * 4u);
+            const auto wt = buf_rsrc(g_eotw[0], 4096u * 8u);
             // the even wave's buffer gets A, the odd wave's B (every j')
             sfor<32>([&](auto J) { buf[64 * J + lane] = v[J]; });
             eo_signal(myflag, step + 1);
@@ -180,11 +157,11 @@ __global__ __launch_bounds__(EO::BG::NT, EO::BG::OCC) void k_ntt_fwd_eo(const ui
                 xb[I] = shoup_mul<P::Q>(xb[I], lam.x, lam.y);
                 ct_bfly<P::Q>(xa[I], xb[I], mu.x, mu.y);
 #else
-                const uint2 tw = eo_ldtw(wt, 8u * lo, 8u * BG::boff(c, I));
+                const uint2 tw = buf_ld2(wt, 8u * lo, 8u * BG::boff(c, I));
                 ct_bfly<P::Q>(xa[I], xb[I], tw.x, tw.y);
 #endif
-                eo_st<EO_POL_C>(canon4<P>(xa[I]), dst, 4u * lo, 4u * BG::boff(c, I));
-                eo_st<EO_POL_C>(canon4<P>(xb[I]), dst, 4u * lo, 4u * (BG::boff(c, I) + EO::HN));
+                buf_st<EO_POL_C>(canon4<P>(xa[I]), dst, 4u * lo, 4u * BG::boff(c, I));
+                buf_st<EO_POL_C>(canon4<P>(xb[I]), dst, 4u * lo, 4u * (BG::boff(c, I) + EO::HN));
             });
             eo_wait(pflag, step + 2);   // before the next transpose rewrites this wave's buffer
             step += 2;
@@ -218,11 +195,11 @@ __global__ __launch_bounds__(EO::BG::NT, EO::BG::OCC) void k_ntt_inv_eo(const ui
     auto load = [&](uint32_t q) __attribute__((always_inline)) {
         uint32_t lo = 128u * par + lane;
         asm volatile("" : "+v"(lo));
-        const auto src = eo_rsrc(in + (size_t)q * EO::N, q < npoly ? EO::N * 4u : 0u);
+        const auto src = buf_rsrc(in + (size_t)q * EO::N, q < npoly ? EO::N * 4u : 0u);
         sfor<2>([&](auto C) {
             sfor<16>([&](auto I) {
-                r[32 * C + I] = eo_ld<EO_POL_C>(src, 4u * lo, 4u * BG::boff(C, I));
-                r[32 * C + 16 + I] = eo_ld<EO_POL_C>(src, 4u * lo, 4u * (BG::boff(C, I) + EO::HN));
+                r[32 * C + I] = buf_ld<EO_POL_C>(src, 4u * lo, 4u * BG::boff(C, I));
+                r[32 * C + 16 + I] = buf_ld<EO_POL_C>(src, 4u * lo, 4u * (BG::boff(C, I) + EO::HN));
             });
         });
     };
@@ -235,7 +212,7 @@ __global__ __launch_bounds__(EO::BG::NT, EO::BG::OCC) void k_ntt_inv_eo(const ui
             constexpr int c = C;
             uint32_t lo = 128u * par + lane;   // natural k = boff(c, I) + lo (see the forward)
             asm volatile("" : "+v"(lo));
-            const auto wt = eo_rsrc(g_eotw[1], 4096u * 8u);
+            const auto wt = buf_rsrc(g_eotw[1], 4096u * 8u);
             sfor<16>([&](auto I) {
                 uint32_t a = r[32 * c + I], b = r[32 * c + 16 + I];
 #if EO_TWJIT
@@ -243,7 +220,7 @@ __global__ __launch_bounds__(EO::BG::NT, EO::BG::OCC) void k_ntt_inv_eo(const ui
                 gs_bfly<EO::P::Q>(a, b, mu.x, mu.y);
                 b = shoup_mul<EO::P::Q>(b, lam.x, lam.y);
 #else
-                const uint2 tw = eo_ldtw(wt, 8u * lo, 8u * BG::boff(c, I));
+                const uint2 tw = buf_ld2(wt, 8u * lo, 8u * BG::boff(c, I));
                 gs_bfly<EO::P::Q>(a, b, tw.x, tw.y);   // A = X[k] + X[k + 4096], B = (X[k] - X[k + 4096]) w^-1
 #endif
                 buf[64 * I + lane] = a;                 // own buffer: A rows 0..15, B rows 16..31
@@ -263,9 +240,9 @@ __global__ __launch_bounds__(EO::BG::NT, EO::BG::OCC) void k_ntt_inv_eo(const ui
         };
         uint32_t lo = 2u * lane + par;   // x[2 (64 J + lane) + par]
         asm volatile("" : "+v"(lo));
-        const auto dst = eo_rsrc(out + (size_t)p * EO::N, EO::N * 4u);
+        const auto dst = buf_rsrc(out + (size_t)p * EO::N, EO::N * 4u);
         big_inv_to<BG, 0, false, EO::S0, EO::S1>(r, buf, tab, h, lane, source, [&](auto J, uint32_t x) __attribute__((always_inline)) {
-            eo_st<EO_POL_S2>(x, dst, 4u * lo, 4u * 128u * (uint32_t)J);
+            buf_st<EO_POL_S2>(x, dst, 4u * lo, 4u * 128u * (uint32_t)J);
         });
         p += EO::NPAIR;
         if (it + 1 < ppw && p < npoly) load(p);

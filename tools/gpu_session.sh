@@ -156,6 +156,11 @@ for step in "${steps[@]}"; do
               run ab11_chk 300 python tools/ab.py $L --param p-III-8192 --batch 40001 --ops fwd,inv --rounds 2 &&
               run ab11_8192 300 python tools/ab.py $L --param p-III-8192 --batch 262144 --ops fwd,inv --inplace --rounds 9 &&
               run ab11_8192s 300 python tools/ab.py $L --param p-III-8192 --batch 65536 --ops fwd,inv --inplace --rounds 15 ;;
+        # round 6: n = 8192 transforms with buffer-resource accesses at 8 / 12 waves
+        ab12) L="ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so ntt-gpu-qtesla_amd/lib/ab12/*.so";
+              run ab12_chk 300 python tools/ab.py $L --param p-III-8192 --batch 40001 --ops fwd,inv,fwdbr,invbr --rounds 2 &&
+              run ab12_8192 300 python tools/ab.py $L --param p-III-8192 --batch 262144 --ops fwd,inv --inplace --rounds 9 &&
+              run ab12_8192s 300 python tools/ab.py $L --param p-III-8192 --batch 65536 --ops fwd,inv --inplace --rounds 15 ;;
         sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
