@@ -161,6 +161,13 @@ for step in "${steps[@]}"; do
               run ab12_chk 300 python tools/ab.py $L --param p-III-8192 --batch 40001 --ops fwd,inv,fwdbr,invbr --rounds 2 &&
               run ab12_8192 300 python tools/ab.py $L --param p-III-8192 --batch 262144 --ops fwd,inv --inplace --rounds 9 &&
               run ab12_8192s 300 python tools/ab.py $L --param p-III-8192 --batch 65536 --ops fwd,inv --inplace --rounds 15 ;;
+        # round 6: radix-16 small-batch kernels with the register budget of 7 / 8 waves per SIMD
+        ab13) L="ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so ntt-gpu-qtesla_amd/lib/ab13/*.so";
+              run ab13_chk 300 python tools/ab.py $L --param p-I --batch 65537 --ops fwd,inv,fwdbr,invbr --rounds 2 &&
+              run ab13_c2 300 python tools/ab.py $L --param p-I --batch 65536 --ops fwd,inv --inplace --rounds 31 &&
+              run ab13_p1 300 python tools/ab.py $L --param p-I --batch 1048576 --ops fwd,inv --inplace --rounds 9 &&
+              run ab13_4096 300 python tools/ab.py $L --param p-III-4096 --batch 16384 --ops fwd,inv --inplace --rounds 31 &&
+              run ab13_8192 300 python tools/ab.py $L --param p-III-8192 --batch 32768 --ops fwd,inv --inplace --rounds 31 ;;
         sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
