@@ -309,13 +309,14 @@ def pattern_floor(args, ntt_amd, torch, x, stream, steps: int):
     kernel family the line's launches run (tools-only diagnostic library,
     tools/ntt_diag.hip: ntt_debug_variant op 0/1 variant 3 for the batch
     kernels, op 5/6 variant 1/5 for the radix-8/16 one-polynomial-per-workgroup
-    kernels), timed in this process AFTER the timed region on the same buffer
+    kernels, op 7 variant 1/3 for the n = 4096 / 8192 one-wave kernels), timed
+    in this process AFTER the timed region on the same buffer
     (its contents no longer matter), with an event pair around `steps`
     back-to-back launches on the kernels' stream.  It is the access pattern's
     own floor: kernel / floor says how much the arithmetic costs the memory
     stream.  Never part of `value`."""
     import ctypes
-    if args.op not in ("fwdinv", "fwd", "inv") or ntt_amd.param_info(args.param)["n"] > 2048:
+    if args.op not in ("fwdinv", "fwd", "inv"):
         return None
     if not os.path.exists(DIAG_PATH):
         return {"note": f"{os.path.relpath(DIAG_PATH, ROOT)} not built (make -C ntt-gpu-qtesla_amd tools)"}
@@ -324,7 +325,10 @@ def pattern_floor(args, ntt_amd, torch, x, stream, steps: int):
     variants = {}
     for k in kinds:
         radix = ntt_amd.small_batch_radix(args.param, k, npoly)
-        if radix == 0:
+        if radix == 0 and ntt_amd.param_info(args.param)["n"] > 2048:
+            variants[k] = (7, 1 if k == "fwd" else 3,
+                           f"k_big_mem<PS, {'false' if k == 'fwd' else 'true'}> (loads + chunk LDS transposes + stores)")
+        elif radix == 0:
             variants[k] = (0 if k == "fwd" else 1, 3, "k_variant<PS, INV, 3> (loads + LDS transpose + stores)")
         elif radix in (8, 16):
             variants[k] = (5 if radix == 8 else 6, 1 if k == "fwd" else 5,

@@ -20,6 +20,11 @@
 //              exchanges and barriers, stores), arithmetic + twiddle loads +
 //              LDS only (no global data traffic), memory only plus the twiddle
 //              loads
+//   op 7       the n = 4096 / 8192 one-wave-per-polynomial transforms
+//              (csrc/ntt_big.hpp, param sets 3 / 4, natural order): variant 0
+//              / 2 the forward / inverse kernels, 1 / 3 their memory-only
+//              variants (the same launch shape, loads, per-chunk LDS
+//              transposes and stores, no arithmetic)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -81,6 +86,65 @@ __global__ __launch_bounds__(NTT_WG, NTT_WAVES_PER_SIMD) void k_variant(const ui
         }
     };
     chunk_loop<NTT_WAVES>(nunits, ppw, prologue, load, process);
+}
+
+// memory-only n = 4096 / 8192 transforms: k_ntt_fwd_big / k_ntt_inv_big's
+// launch, table prologue, loads, chunk transposes and stores, without the
+// butterflies, the bit-5 swap or the twiddle reads
+template <int PS, bool INV>
+__global__ __launch_bounds__(Big<PS>::NT, Big<PS>::OCC) void k_big_mem(const uint32_t *in, uint32_t *out, uint32_t npoly,
+                                                                    uint32_t ppw)
+{
+    using BG = Big<PS>;
+    using P = typename BG::P;
+    constexpr uint32_t N = BG::PL::N;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BG::LDS_WORDS];
+    uint32_t *const tabw = lds + BG::WAVES * XPOSE_WORDS;
+    auto prologue = [&]() {
+        fill_big_tw<BG, INV>(tabw);
+        __syncthreads();
+    };
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t *const buf = lds + (threadIdx.x >> 6) * XPOSE_WORDS;
+    auto load = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
+        if constexpr (!INV) big_load_a<BG>(r, in + (size_t)u * N, lane);
+        else big_load_b<BG>(r, in + (size_t)u * N, lane);
+    };
+    auto process = [&](uint32_t (&r)[BG::R], uint32_t u) __attribute__((always_inline)) {
+        uint32_t lo = lane;
+        asm volatile("" : "+v"(lo));
+        uint32_t *const dst = out + (size_t)u * N + lo;
+        sfor<BG::CH>([&](auto C) {
+            const uint32_t wb = big_wbase(opaque_lane());
+            const Lane<P> LB(opaque_lane());
+            if constexpr (!INV) {   // A'' rows -> b128 reads of layout B -> B-order stores
+                sfor<32>([&](auto T) { buf[big_waddr(wb, T)] = r[BG::creg(C, T)]; });
+                compiler_fence();
+                uint32_t v[32];
+                sfor<8>([&](auto Q) {
+                    const uint4 x = *reinterpret_cast<const uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm));
+                    v[4 * Q + 0] = x.x;
+                    v[4 * Q + 1] = x.y;
+                    v[4 * Q + 2] = x.z;
+                    v[4 * Q + 3] = x.w;
+                });
+                compiler_fence();
+                sfor<32>([&](auto JP) { st_out(dst + BG::boff(C, JP), v[JP]); });
+            } else {   // layout B -> b128 writes -> A'' rows back into the registers
+                sfor<8>([&](auto Q) {
+                    *reinterpret_cast<uint4 *>(buf + LB.rbase + ((4u * Q) ^ LB.rxm)) =
+                        make_uint4(r[BG::creg(C, 4 * Q + 0)], r[BG::creg(C, 4 * Q + 1)], r[BG::creg(C, 4 * Q + 2)],
+                                   r[BG::creg(C, 4 * Q + 3)]);
+                });
+                compiler_fence();
+                sfor<32>([&](auto T) { r[BG::creg(C, T)] = buf[big_waddr(wb, T)]; });
+                compiler_fence();
+            }
+        });
+        if constexpr (INV)   // layout A stores (lane-contiguous 256-B runs)
+            sfor<BG::R>([&](auto J) { st_out(dst + 64u * (uint32_t)J, r[J]); });
+    };
+    big_loop<BG>(npoly, ppw, prologue, load, process);
 }
 
 template <int W>
@@ -159,7 +223,7 @@ extern "C" int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uin
                                  void *stream)
 {
     const ParamSet *p = param_set(ps);
-    if (!p || ps > 2) return NTT_ERR_PARAM;   // the n = 4096 / 8192 sets have no variants here
+    if (!p || (ps > 2) != (op == 7)) return NTT_ERR_PARAM;   // op 7: the n = 4096 / 8192 sets only
     if (batch == 0) return NTT_OK;
     if (!d_in || !d_out) return NTT_ERR_NULL;
     if ((((uintptr_t)d_in) | ((uintptr_t)d_out)) & 15u) return NTT_ERR_ALIGN;
@@ -203,6 +267,25 @@ extern "C" int ntt_debug_variant(int op, int variant, uint32_t *d_out, const uin
         default: return NTT_ERR_PARAM;
         }
         return hipGetLastError() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    }
+    if (op == 7) {   // n = 4096 / 8192: the library's launch shape (ntt_kernels.hip, LXform)
+        auto run = [&](auto PSI) {
+            constexpr int PS = decltype(PSI)::value;
+            using BG = Big<PS>;
+            size_t ppw = batch / ((size_t)BG::WAVES * g_cus * 2);
+            ppw = ppw < 1 ? 1 : (ppw > 16 ? 16 : ppw);
+            const dim3 g((uint32_t)((batch + BG::WAVES * ppw - 1) / (BG::WAVES * ppw))), b(BG::NT);
+            const uint32_t nb = (uint32_t)batch, pw = (uint32_t)ppw;
+            switch (variant) {
+            case 0: hipLaunchKernelGGL((k_ntt_fwd_big<PS, false>), g, b, 0, s, d_in, d_out, nb, pw); break;
+            case 1: hipLaunchKernelGGL((k_big_mem<PS, false>), g, b, 0, s, d_in, d_out, nb, pw); break;
+            case 2: hipLaunchKernelGGL((k_ntt_inv_big<PS, false>), g, b, 0, s, d_in, d_out, nb, pw); break;
+            case 3: hipLaunchKernelGGL((k_big_mem<PS, true>), g, b, 0, s, d_in, d_out, nb, pw); break;
+            default: return (int)NTT_ERR_PARAM;
+            }
+            return hipGetLastError() == hipSuccess ? (int)NTT_OK : (int)NTT_ERR_HIP;
+        };
+        return ps == 3 ? run(std::integral_constant<int, 3>{}) : run(std::integral_constant<int, 4>{});
     }
     if (op == 5 || op == 6) {   // one polynomial per workgroup: the grid is the batch
         const dim3 g((uint32_t)batch);
