@@ -168,6 +168,12 @@ for step in "${steps[@]}"; do
               run ab13_p1 300 python tools/ab.py $L --param p-I --batch 1048576 --ops fwd,inv --inplace --rounds 9 &&
               run ab13_4096 300 python tools/ab.py $L --param p-III-4096 --batch 16384 --ops fwd,inv --inplace --rounds 31 &&
               run ab13_8192 300 python tools/ab.py $L --param p-III-8192 --batch 32768 --ops fwd,inv --inplace --rounds 31 ;;
+        # round 6: software-pipelined n = 4096 / 8192 transforms (BIG_PF)
+        ab14) L="ntt-gpu-qtesla_amd/lib/libqtesla_ntt.so ntt-gpu-qtesla_amd/lib/ab14/*.so";
+              run ab14_chk8 300 python tools/ab.py $L --param p-III-8192 --batch 40001 --ops fwd,inv --rounds 2 &&
+              run ab14_chk4 300 python tools/ab.py $L --param p-III-4096 --batch 40001 --ops fwd,inv --rounds 2 &&
+              run ab14_8192 300 python tools/ab.py $L --param p-III-8192 --batch 262144 --ops fwd,inv --inplace --rounds 9 &&
+              run ab14_4096 300 python tools/ab.py $L --param p-III-4096 --batch 524288 --ops fwd,inv --inplace --rounds 9 ;;
         sweepbr) run sweepbr 600 python tools/switch_sweep.py ntt-gpu-qtesla_amd/lib/sweep/a_batch.so ntt-gpu-qtesla_amd/lib/sweep/b_lat.so --params p-III-4096,p-III-8192 --ops fwdbr,invbr --out gpurun_out/switch_sweep_br.json ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
