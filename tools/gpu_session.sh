@@ -103,6 +103,12 @@ for step in "${steps[@]}"; do
         # SQ_INSTS_VALU + GRBM_GUI_ACTIVE per launch of a config's kernel
         valucost) run valucost 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU --output-format csv -d gpurun_out/valucost -o run -- ./ntt-gpu-qtesla_amd/bin/valu_cost 16384 ;;
         valum_*) n=${step#valum_}; b=$((1073741824 / n)); run valum_$n 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valum_$n -o run -- python3 bench.py --op polymul --param p-III-$n --batch $b --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
+        # round 6: poly_mul_ntt's own FETCH / WRITE and VALU passes and its bench line alone
+        pmcmn_*) n=${step#pmcmn_}; b=$((1073741824 / n)); a="--op polymul_ntt --param p-III-$n --batch $b --steps 3 --warmup 1 --no-cpu-baseline --no-check";
+                 run pmcmn_${n}_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcmn_${n}_fetch -o run -- python3 bench.py $a &&
+                 run pmcmn_${n}_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcmn_${n}_write -o run -- python3 bench.py $a ;;
+        valumn_*) n=${step#valumn_}; b=$((1073741824 / n)); run valumn_$n 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valumn_$n -o run -- python3 bench.py --op polymul_ntt --param p-III-$n --batch $b --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
+        benchmnx_*) n=${step#benchmnx_}; b=$((1073741824 / n)); run benchmn_$n 300 python bench.py --op polymul_ntt --param p-III-$n --batch $b --steps 20 --warmup 3 --cpu-seconds 5 ;;
         valu_c*) c=${step#valu_c}; run valu_c$c 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valu_c$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
         # round 6: the small-batch switch per (n, op): latency vs batch kernels
         # from 64 polynomials to the BASELINE batches (tools/switch_sweep.py)
