@@ -26,6 +26,11 @@ done
 for n in 4096 8192; do
     cp $S/profl_$n/run_kernel_stats.csv "$D/rocprof_kernel_stats_l_$n.csv"
     cp $S/profm_$n/run_kernel_stats.csv "$D/rocprof_kernel_stats_m_$n.csv"
+    mkdir -p "$D/pmcmn_$n" "$D/valumn_$n" "$D/valum_$n"
+    cp $S/pmcmn_${n}_fetch/run_counter_collection.csv "$D/pmcmn_$n/fetch_counter_collection.csv"
+    cp $S/pmcmn_${n}_write/run_counter_collection.csv "$D/pmcmn_$n/write_counter_collection.csv"
+    cp $S/valum_$n/run_counter_collection.csv "$D/valum_$n/"
+    cp $S/valumn_$n/run_counter_collection.csv "$D/valumn_$n/"
     for k in l m; do
         mkdir -p "$D/pmc${k}_$n"
         cp $S/pmc${k}_${n}_fetch/run_counter_collection.csv "$D/pmc${k}_$n/fetch_counter_collection.csv"

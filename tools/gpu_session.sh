@@ -23,7 +23,8 @@ for step in "$@"; do
     case $step in
         final) steps+=(pytest smoke bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 benchl_4096 benchl_8192 benchm_4096 benchm_8192
                        prof_c2 prof_c3 prof_c4 prof_c5 profl_4096 profl_8192 profm_4096 profm_8192
-                       pmc_c2 pmc_c3 pmc_c4 pmc_c5 pmcl_4096 pmcl_8192 pmcm_4096 pmcm_8192 valu_c4 valu_c5 valum_4096 valum_8192 sq_c5 sqb_c5) ;;
+                       pmc_c2 pmc_c3 pmc_c4 pmc_c5 pmcl_4096 pmcl_8192 pmcm_4096 pmcm_8192 pmcmn_4096 pmcmn_8192
+                       valu_c4 valu_c5 valum_4096 valum_8192 valumn_4096 valumn_8192 sq_c5 sqb_c5) ;;
         verify) steps+=(bench_c2 bench_c3 bench_c4 bench_c5 benchl_4096 benchl_8192 benchm_4096 benchm_8192) ;;
         *) steps+=("$step") ;;
     esac
@@ -106,7 +107,8 @@ for step in "${steps[@]}"; do
         # round 6: poly_mul_ntt's own FETCH / WRITE and VALU passes and its bench line alone
         pmcmn_*) n=${step#pmcmn_}; b=$((1073741824 / n)); a="--op polymul_ntt --param p-III-$n --batch $b --steps 3 --warmup 1 --no-cpu-baseline --no-check";
                  run pmcmn_${n}_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcmn_${n}_fetch -o run -- python3 bench.py $a &&
-                 run pmcmn_${n}_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcmn_${n}_write -o run -- python3 bench.py $a ;;
+                 run pmcmn_${n}_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcmn_${n}_write -o run -- python3 bench.py $a &&
+                 run pmcmn_${n}_sum 60 python3 tools/pmc_summary.py --op polymul_ntt --param p-III-$n --batch $b --fetch gpurun_out/pmcmn_${n}_fetch/run_counter_collection.csv --write gpurun_out/pmcmn_${n}_write/run_counter_collection.csv --out gpurun_out/pmc_summary.json ;;
         valumn_*) n=${step#valumn_}; b=$((1073741824 / n)); run valumn_$n 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valumn_$n -o run -- python3 bench.py --op polymul_ntt --param p-III-$n --batch $b --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
         benchmnx_*) n=${step#benchmnx_}; b=$((1073741824 / n)); run benchmn_$n 300 python bench.py --op polymul_ntt --param p-III-$n --batch $b --steps 20 --warmup 3 --cpu-seconds 5 ;;
         valu_c*) c=${step#valu_c}; run valu_c$c 120 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/valu_c$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-check ;;
