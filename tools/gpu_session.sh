@@ -74,7 +74,9 @@ for step in "${steps[@]}"; do
         # (20 / 200 / 1000 steps: 0.116 / 0.119 / 0.111 ms, profiles/r03/c2/steps.log)
         # config 1 (one polynomial per call, ~5-8 us of Python submission each) likewise
         bench_c*) c=${step#bench_c}; k=20; [ "$c" = 2 ] || [ "$c" = 1 ] && k=1000; run bench_c$c 500 python bench.py --config $c --steps $k --warmup 3 --cpu-seconds 10 ;;
-        prof_c*) c=${step#prof_c}; run prof_c$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c$c -o run -- python3 bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-check ;;
+        # rocprofv3 averages include the warm-up launches (clock ramp): 100 timed
+        # steps (config 2: 1000, like its bench line) keep them a small share
+        prof_c*) c=${step#prof_c}; k=100; [ "$c" = 2 ] && k=1000; run prof_c$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c$c -o run -- python3 bench.py --config $c --steps $k --warmup 3 --no-cpu-baseline --no-check ;;
         pmc_c*) c=${step#pmc_c}; run pmc_c${c}_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_c${c}_fetch -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-check &&
                  run pmc_c${c}_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_c${c}_write -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-check &&
                  run pmc_c${c}_sum 60 python3 tools/pmc_summary.py --config $c --fetch gpurun_out/pmc_c${c}_fetch/run_counter_collection.csv --write gpurun_out/pmc_c${c}_write/run_counter_collection.csv --out gpurun_out/pmc_summary.json ;;
@@ -88,8 +90,8 @@ for step in "${steps[@]}"; do
                 run pmcm_${n}_sum 60 python3 tools/pmc_summary.py --op polymul --param p-III-$n --batch $b --fetch gpurun_out/pmcm_${n}_fetch/run_counter_collection.csv --write gpurun_out/pmcm_${n}_write/run_counter_collection.csv --out gpurun_out/pmc_summary.json ;;
         benchm_*) n=${step#benchm_}; b=$((1073741824 / n)); run benchm_$n 300 python bench.py --op polymul --param p-III-$n --batch $b --steps 20 --warmup 3 --cpu-seconds 5 &&
                   run benchmn_$n 300 python bench.py --op polymul_ntt --param p-III-$n --batch $b --steps 20 --warmup 3 --cpu-seconds 5 ;;
-        profm_*) n=${step#profm_}; b=$((1073741824 / n)); run profm_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profm_$n -o run -- python3 bench.py --op polymul --param p-III-$n --batch $b --steps 20 --warmup 3 --no-cpu-baseline --no-check ;;
-        profl_*) n=${step#profl_}; b=$((8589934592 / 4 / n)); run profl_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profl_$n -o run -- python3 bench.py --op fwdinv --param p-III-$n --batch $b --steps 20 --warmup 3 --no-cpu-baseline --no-check ;;
+        profm_*) n=${step#profm_}; b=$((1073741824 / n)); run profm_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profm_$n -o run -- python3 bench.py --op polymul --param p-III-$n --batch $b --steps 100 --warmup 3 --no-cpu-baseline --no-check ;;
+        profl_*) n=${step#profl_}; b=$((8589934592 / 4 / n)); run profl_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profl_$n -o run -- python3 bench.py --op fwdinv --param p-III-$n --batch $b --steps 100 --warmup 3 --no-cpu-baseline --no-check ;;
         benchl_*) n=${step#benchl_}; b=$((8589934592 / 4 / n)); run benchl_$n 300 python bench.py --op fwdinv --param p-III-$n --batch $b --steps 20 --warmup 3 --cpu-seconds 5 ;;
         sq_c*) c=${step#sq_c}; run sq_c$c 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sq_c$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-check ;;
         sqb_c*) c=${step#sqb_c}; run sqb_c$c 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM --output-format csv -d gpurun_out/sqb_c$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-check ;;
