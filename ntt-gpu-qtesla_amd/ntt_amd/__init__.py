@@ -294,11 +294,11 @@ def _inplace(name: str, t, param_set, stream):
     ps = PARAM_SETS[param_set] if isinstance(param_set, str) else int(param_set)
     dev = t.get_device()
     if torch.cuda.current_device() == dev:
-        s = torch.cuda.current_stream(dev).cuda_stream if stream is None else getattr(stream, "cuda_stream", stream)
+        s = _current_raw_stream(dev) if stream is None else getattr(stream, "cuda_stream", stream)
         rc = fn(t.data_ptr(), None, numel // n, ps, s)
     else:
         with torch.cuda.device(dev):
-            s = torch.cuda.current_stream(dev).cuda_stream if stream is None else getattr(stream, "cuda_stream", stream)
+            s = _current_raw_stream(dev) if stream is None else getattr(stream, "cuda_stream", stream)
             rc = fn(t.data_ptr(), None, numel // n, ps, s)
     if rc != NTT_OK:
         raise NTTError(rc, name)
@@ -306,6 +306,16 @@ def _inplace(name: str, t, param_set, stream):
 
 
 _FN: dict = {}
+
+
+def _current_raw_stream(dev: int):
+    """The device's current stream handle as an int: torch's raw accessor
+    where this torch build has it (no Stream object: ~1.4 us less per call,
+    tools/call_overhead.py), else the public current_stream()."""
+    raw = getattr(_TORCH._C, "_cuda_getCurrentRawStream", None)
+    if raw is not None:
+        return raw(dev)
+    return _TORCH.cuda.current_stream(dev).cuda_stream
 
 
 def poly_ntt(t, param_set, stream=None):
