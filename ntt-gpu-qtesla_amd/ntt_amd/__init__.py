@@ -236,7 +236,10 @@ def _device_of(*tensors):
 
 def _stream(stream, device=None):
     if stream is None:
-        return _torch().cuda.current_stream(device).cuda_stream
+        torch = _torch()
+        if isinstance(device, torch.device) and device.index is not None:
+            return _current_raw_stream(device.index)
+        return torch.cuda.current_stream(device).cuda_stream
     return getattr(stream, "cuda_stream", stream)
 
 
